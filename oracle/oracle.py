@@ -1,0 +1,90 @@
+"""ctypes wrapper around oracle/_build/libpolar_oracle.so (CPU restatement of the reference).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg as the checker.  The product decoders (polar_amd) never import this module.
+Pinned against tests/golden/*.npz by tests/test_oracle.py.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libpolar_oracle.so")
+_lib = None
+
+
+def build(force=False):
+    """Compile the oracle with gcc (make in oracle/)."""
+    src = os.path.join(_HERE, "polar_oracle.c")
+    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", _HERE], stdout=subprocess.DEVNULL)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(_LIB_PATH)
+        P = ctypes.c_void_p
+        i32, i64 = ctypes.c_int, ctypes.c_int64
+        L.orc_sc_decode.argtypes = [i32, P, i32, P, i64, P, i32]
+        L.orc_scl_decode.argtypes = [i32, P, i32, P, i64, P, P, i32]
+        L.orc_scl_decode_lazy.argtypes = [i32, P, i32, P, i64, P, P, i32]
+        L.orc_polar_encode.argtypes = [i32, P, P, i64, P]
+        for f in (L.orc_sc_decode, L.orc_scl_decode, L.orc_scl_decode_lazy, L.orc_polar_encode):
+            f.restype = i32
+        _lib = L
+    return _lib
+
+
+def frozen_mask(frozen_pos, n):
+    m = np.zeros(n, dtype=np.uint8)
+    m[np.asarray(frozen_pos, dtype=np.int64)] = 1
+    return m
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def sc_decode(llr_logits, frozen_pos, f_mode=0, nthreads=0):
+    """SC decode (polar_sc.py SC_Dec semantics).  llr_logits: [bs, n] float32 logits.
+    Returns float32 [bs, k] 0/1 bits."""
+    x = np.ascontiguousarray(llr_logits, dtype=np.float32)
+    bs, n = x.shape
+    fm = frozen_mask(frozen_pos, n)
+    k = int(n - fm.sum())
+    out = np.empty((bs, k), dtype=np.float32)
+    r = lib().orc_sc_decode(n, _ptr(fm), int(f_mode), _ptr(x), bs, _ptr(out), int(nthreads))
+    if r < 0:
+        raise ValueError("orc_sc_decode rejected its arguments")
+    return out
+
+
+def scl_decode(llr_logits, frozen_pos, list_size=8, nthreads=0, lazy=False):
+    """SCL decode (polar_scl.py SCL_Dec semantics, stable tie order).
+    Returns (bits float32 [bs,k], sorted msg_pm float64 [bs, 2L])."""
+    x = np.ascontiguousarray(llr_logits, dtype=np.float32)
+    bs, n = x.shape
+    fm = frozen_mask(frozen_pos, n)
+    k = int(n - fm.sum())
+    out = np.empty((bs, k), dtype=np.float32)
+    pm = np.empty((bs, 2 * list_size), dtype=np.float64)
+    fn = lib().orc_scl_decode_lazy if lazy else lib().orc_scl_decode
+    r = fn(n, _ptr(fm), int(list_size), _ptr(x), bs, _ptr(out), _ptr(pm), int(nthreads))
+    if r < 0:
+        raise ValueError("orc_scl_decode rejected its arguments")
+    return out, pm
+
+
+def polar_encode(u_bits, frozen_pos, n):
+    """Polar encoding (x_run enc.py semantics).  u_bits: [bs, k] 0/1 -> float32 [bs, n]."""
+    u = np.ascontiguousarray(u_bits, dtype=np.float32)
+    bs = u.shape[0]
+    fm = frozen_mask(frozen_pos, n)
+    out = np.empty((bs, n), dtype=np.float32)
+    lib().orc_polar_encode(n, _ptr(fm), _ptr(u), bs, _ptr(out))
+    return out
