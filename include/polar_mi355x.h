@@ -1,0 +1,82 @@
+/*
+ * polar_mi355x.h -- C ABI of the MI355X (gfx950) SC / SC-list polar decoder library.
+ *
+ * This is the drop-in boundary for the hot path named in BASELINE.json: the Python decoder
+ * modules (polar_amd.SC_Dec / SCL_Dec, mirroring the reference constructors and forward())
+ * call these entry points through ctypes.  All pointers are device pointers unless a comment
+ * says otherwise; the caller (PyTorch) owns every buffer; launches are asynchronous and
+ * ordered on the given hipStream_t (passed as void*; NULL = legacy default stream).
+ * No exceptions cross this boundary: 0 = success, negative = error, details from
+ * pl_last_error_string() (thread-local).
+ *
+ * Reference interfaces replaced (jaco267/polar-code-pytorch-sionna):
+ *   pl_plan_create   SC_Dec.__init__   x_run_sn_polar/polar/polar_sc.py:10-32
+ *                    SCL_Dec.__init__  x_run_sn_polar/polar/polar_scl.py:13-42
+ *                    (my_sn/fec/polar/dec.py:18-31 and :183-242 for the exact-f variants)
+ *   pl_sc_decode     SC_Dec.forward    x_run_sn_polar/polar/polar_sc.py:113-133
+ *                    (f_mode=PL_F_EXACT: my_sn/fec/polar/dec.py:130-157)
+ *   pl_scl_decode    SCL_Dec.forward   x_run_sn_polar/polar/polar_scl.py:210-234
+ *                    (+ final sorted msg_pm of _decode_np_batch :178-209)
+ *   pl_polar_encode  PolarEncoder.forward x_run_sn_polar/polar/enc.py:30-43
+ *                    (butterfly form of my_sn/fec/polar/enc.py:85-96)
+ */
+#ifndef POLAR_MI355X_H
+#define POLAR_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PL_OK 0
+#define PL_EINVAL -1  /* bad argument / shape */
+#define PL_EHIP -2    /* HIP runtime error */
+#define PL_ENOTSUP -3 /* configuration not supported by this build */
+
+#define PL_F_MINSUM 0 /* f = sign*sign*min(|x|,|y|) on clipped inputs (polar_sc.py:46) */
+#define PL_F_EXACT 1  /* f = log(1+e^(x+y)) - log(e^x+e^y) (my_sn dec.py:39-43) */
+
+#define PL_OUT_F32 0  /* output 0.0f/1.0f floats, [bs, k] (reference output dtype) */
+#define PL_OUT_U8 1   /* output 0/1 bytes, [bs, k] */
+
+typedef struct pl_plan pl_plan;
+
+/* Build an immutable decoding plan for a length-n polar code.
+ * frozen_mask: HOST pointer to n bytes, nonzero = frozen position (frozen_pos of the reference).
+ * list_size:   1 for SC plans; a power of two <= 32 for SCL plans.
+ * f_mode:      PL_F_MINSUM or PL_F_EXACT.  llr_max: clipping bound (reference: 30).
+ * flags:       reserved, pass 0.
+ * n must be a power of two, 2 <= n <= 2048 (SC) / 2 <= n <= 1024 (SCL). */
+int pl_plan_create(pl_plan** out, int32_t n, const uint8_t* frozen_mask, int32_t list_size,
+                   int32_t f_mode, float llr_max, uint32_t flags);
+int pl_plan_destroy(pl_plan* plan);
+/* n, k (information bits) and list size of a plan (any pointer may be NULL). */
+int pl_plan_info(const pl_plan* plan, int32_t* n, int32_t* k, int32_t* list_size);
+
+/* SC decode.  llr_logits: [bs, n] fp32 logits log(P(b=1)/P(b=0)) (NOT negated; the decoder
+ * negates, polar_sc.py:122).  out_bits: [bs, k] decided information bits at info_pos ascending,
+ * dtype per out_kind (PL_OUT_F32 / PL_OUT_U8). */
+int pl_sc_decode(const pl_plan* plan, const float* llr_logits, int64_t bs, void* out_bits,
+                 int32_t out_kind, void* hip_stream);
+
+/* SCL decode.  out_pm (nullable): [bs, 2L] fp64, the reference's final sorted msg_pm.
+ * workspace: device scratch of pl_scl_workspace_size(plan, bs) bytes (may be NULL when that
+ * size is 0). */
+size_t pl_scl_workspace_size(const pl_plan* plan, int64_t bs);
+int pl_scl_decode(const pl_plan* plan, const float* llr_logits, int64_t bs, void* out_bits,
+                  int32_t out_kind, double* out_pm, void* workspace, size_t ws_bytes,
+                  void* hip_stream);
+
+/* Polar encoding with the plan's frozen set: u_bits [bs, k] fp32 0/1 -> codewords [bs, n] fp32. */
+int pl_polar_encode(const pl_plan* plan, const float* u_bits, int64_t bs, float* codewords,
+                    void* hip_stream);
+
+const char* pl_last_error_string(void);
+const char* pl_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* POLAR_MI355X_H */

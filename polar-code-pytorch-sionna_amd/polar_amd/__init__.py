@@ -1,0 +1,10 @@
+"""polar_amd -- MI355X-native (gfx950) SC / SC-list polar decoding behind the reference API.
+
+Hot path: libpolar_mi355x.so (hand-written HIP kernels + C ABI, include/polar_mi355x.h).
+Drop-ins: SC_Dec / SCL_Dec (x_run_sn_polar/polar/polar_sc.py, polar_scl.py).
+"""
+from . import _lib, ops  # noqa: F401
+from .decoders import SC_Dec, SCL_Dec  # noqa: F401
+from .frozen import F2, get_Kern_frozen_bits, reference_frozen_pos, frozen_mask  # noqa: F401
+
+__all__ = ["SC_Dec", "SCL_Dec", "F2", "get_Kern_frozen_bits", "reference_frozen_pos", "frozen_mask", "ops"]

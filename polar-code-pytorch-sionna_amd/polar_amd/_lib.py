@@ -1,0 +1,100 @@
+"""ctypes binding of libpolar_mi355x.so (the C ABI in include/polar_mi355x.h).
+
+`import torch` happens before the CDLL load so that libamdhip64.so.7 resolves to the HIP runtime
+torch already loaded (same SONAME), i.e. one runtime, one device context, torch's streams usable
+as hipStream_t.  There is no CPU fallback: if the library or a GPU is missing, every decode call
+raises.
+"""
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (must precede the CDLL load)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpolar_mi355x.so")
+
+PL_OK, PL_EINVAL, PL_EHIP, PL_ENOTSUP = 0, -1, -2, -3
+PL_F_MINSUM, PL_F_EXACT = 0, 1
+PL_OUT_F32, PL_OUT_U8 = 0, 1
+
+_lock = threading.Lock()
+_lib = None
+
+
+class PolarLibError(RuntimeError):
+    pass
+
+
+def _declare(L):
+    P, i32, i64, u32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32
+    L.pl_plan_create.argtypes = [ctypes.POINTER(P), i32, P, i32, i32, ctypes.c_float, u32]
+    L.pl_plan_destroy.argtypes = [P]
+    L.pl_plan_info.argtypes = [P, P, P, P]
+    L.pl_sc_decode.argtypes = [P, P, i64, P, i32, P]
+    L.pl_scl_workspace_size.argtypes = [P, i64]
+    L.pl_scl_workspace_size.restype = ctypes.c_size_t
+    L.pl_scl_decode.argtypes = [P, P, i64, P, i32, P, P, ctypes.c_size_t, P]
+    L.pl_polar_encode.argtypes = [P, P, i64, P, P]
+    L.pl_last_error_string.restype = ctypes.c_char_p
+    L.pl_version.restype = ctypes.c_char_p
+    for f in (L.pl_plan_create, L.pl_plan_destroy, L.pl_plan_info, L.pl_sc_decode, L.pl_scl_decode,
+              L.pl_polar_encode):
+        f.restype = ctypes.c_int
+    return L
+
+
+def lib():
+    """Load (once) and return the ctypes handle.  Raises if the library has not been built."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise PolarLibError(
+                        f"{LIB_PATH} is missing: build it with `python -m polar_amd.build` "
+                        "(hipcc, gfx950).  There is no CPU fallback.")
+                _lib = _declare(ctypes.CDLL(LIB_PATH))
+    return _lib
+
+
+EXPORTED_SYMBOLS = ("pl_plan_create", "pl_plan_destroy", "pl_plan_info", "pl_sc_decode",
+                    "pl_scl_workspace_size", "pl_scl_decode", "pl_polar_encode",
+                    "pl_last_error_string", "pl_version")
+
+
+def check(rc, what):
+    if rc != PL_OK:
+        msg = lib().pl_last_error_string().decode(errors="replace")
+        if rc == PL_EINVAL:
+            raise ValueError(f"{what}: {msg}")
+        raise PolarLibError(f"{what} failed ({rc}): {msg}")
+
+
+def current_stream_ptr(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class Plan:
+    """Owning wrapper of a pl_plan* (immutable, usable from any stream)."""
+
+    def __init__(self, n, frozen_mask_u8, list_size=1, f_mode=PL_F_MINSUM, llr_max=30.0):
+        import numpy as np
+        mask = np.ascontiguousarray(frozen_mask_u8, dtype=np.uint8)
+        assert mask.shape == (n,)
+        self._h = ctypes.c_void_p()
+        check(lib().pl_plan_create(ctypes.byref(self._h), int(n), mask.ctypes.data_as(ctypes.c_void_p),
+                                   int(list_size), int(f_mode), float(llr_max), 0), "pl_plan_create")
+        n_, k_, l_ = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        check(lib().pl_plan_info(self._h, ctypes.byref(n_), ctypes.byref(k_), ctypes.byref(l_)), "pl_plan_info")
+        self.n, self.k, self.list_size = n_.value, k_.value, l_.value
+
+    @property
+    def handle(self):
+        return self._h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value and _lib is not None:
+            _lib.pl_plan_destroy(h)
+            self._h = None

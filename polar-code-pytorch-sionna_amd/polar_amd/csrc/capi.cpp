@@ -1,0 +1,185 @@
+// capi.cpp -- extern "C" boundary of libpolar_mi355x.so (declared in include/polar_mi355x.h).
+//
+// Plan construction mirrors the reference decoder constructors:
+//   SC_Dec.__init__  x_run_sn_polar/polar/polar_sc.py:10-32  (k = n - |frozen|, sorted info_pos)
+//   SCL_Dec.__init__ x_run_sn_polar/polar/polar_scl.py:13-42 (n, list_size powers of two)
+// and precomputes, once, everything the kernels query: the frozen bitmask, the rate-0 node
+// bitmask (all-frozen subtrees, skipped exactly), info_pos and the inverse rank table.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../../include/polar_mi355x.h"
+#include "plan.h"
+
+namespace {
+thread_local std::string g_last_error;
+}
+
+namespace pl {
+void set_error(const std::string& msg) { g_last_error = msg; }
+int check_hip(hipError_t e, const char* what) {
+    if (e == hipSuccess) return PL_OK;
+    set_error(std::string(what) + ": " + hipGetErrorString(e));
+    return PL_EHIP;
+}
+}  // namespace pl
+
+namespace {
+
+int ilog2_exact(int n) {
+    int s = 0;
+    while ((1 << s) < n) ++s;
+    return ((1 << s) == n) ? s : -1;
+}
+
+template <typename T>
+int upload(T** dst, const std::vector<T>& src) {
+    if (src.empty()) return PL_OK;
+    int r = pl::check_hip(hipMalloc(reinterpret_cast<void**>(dst), src.size() * sizeof(T)), "hipMalloc(plan)");
+    if (r) return r;
+    return pl::check_hip(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice), "hipMemcpy(plan)");
+}
+
+void free_plan(pl_plan* p) {
+    if (!p) return;
+    (void)hipFree(p->d_frozen_words);
+    (void)hipFree(p->d_rate0_words);
+    (void)hipFree(p->d_info_pos);
+    (void)hipFree(p->d_info_rank);
+    delete p;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* pl_last_error_string(void) { return g_last_error.c_str(); }
+const char* pl_version(void) { return "polar_mi355x 0.1.0 (gfx950)"; }
+
+int pl_plan_create(pl_plan** out, int32_t n, const uint8_t* frozen_mask, int32_t list_size, int32_t f_mode,
+                   float llr_max, uint32_t flags) {
+    if (!out || !frozen_mask) {
+        pl::set_error("pl_plan_create: null pointer");
+        return PL_EINVAL;
+    }
+    *out = nullptr;
+    const int log_n = ilog2_exact(n);
+    if (log_n < 1 || log_n > 11) {
+        pl::set_error("pl_plan_create: n must be a power of two in [2, 2048]");
+        return PL_EINVAL;
+    }
+    if (list_size < 1 || list_size > 32 || (list_size & (list_size - 1))) {
+        pl::set_error("pl_plan_create: list_size must be a power of two in [1, 32]");
+        return PL_EINVAL;
+    }
+    if (f_mode != PL_F_MINSUM && f_mode != PL_F_EXACT) {
+        pl::set_error("pl_plan_create: unknown f_mode");
+        return PL_EINVAL;
+    }
+    if (!(llr_max > 0.0f)) {
+        pl::set_error("pl_plan_create: llr_max must be positive");
+        return PL_EINVAL;
+    }
+    pl_plan* p = new pl_plan();
+    p->n = n;
+    p->log_n = log_n;
+    p->list_size = list_size;
+    p->f_mode = f_mode;
+    p->llr_max = llr_max;
+    p->flags = flags;
+
+    const int nwords = (n + 31) / 32;
+    std::vector<uint32_t> fw(nwords, 0u);
+    std::vector<int32_t> info, rank(n, -1);
+    for (int i = 0; i < n; ++i) {
+        if (frozen_mask[i]) {
+            fw[i >> 5] |= 1u << (i & 31);
+        } else {
+            rank[i] = (int32_t)info.size();
+            info.push_back(i);
+        }
+    }
+    p->k = (int32_t)info.size();
+    // rate-0 flags: stage s (1..log_n-... all stages), node q = p >> s -> bit OFF(s) + q,
+    // OFF(s) = n - (n >> (s-1)).  Node is rate-0 iff every position in [q*2^s, (q+1)*2^s) is frozen.
+    std::vector<uint32_t> r0(((n - 1) + 31) / 32 + 1, 0u);
+    for (int s = 1; s <= log_n; ++s) {
+        const int off = n - (n >> (s - 1));
+        for (int q = 0; q < (n >> s); ++q) {
+            bool all = true;
+            for (int i = q << s; i < ((q + 1) << s) && all; ++i) all = frozen_mask[i] != 0;
+            if (all) r0[(off + q) >> 5] |= 1u << ((off + q) & 31);
+        }
+    }
+    int r = upload(&p->d_frozen_words, fw);
+    if (!r) r = upload(&p->d_rate0_words, r0);
+    if (!r) r = upload(&p->d_info_rank, rank);
+    if (!r && !info.empty()) r = upload(&p->d_info_pos, info);
+    if (r) {
+        free_plan(p);
+        return r;
+    }
+    *out = p;
+    return PL_OK;
+}
+
+int pl_plan_destroy(pl_plan* plan) {
+    free_plan(plan);
+    return PL_OK;
+}
+
+int pl_plan_info(const pl_plan* p, int32_t* n, int32_t* k, int32_t* list_size) {
+    if (!p) {
+        pl::set_error("pl_plan_info: null plan");
+        return PL_EINVAL;
+    }
+    if (n) *n = p->n;
+    if (k) *k = p->k;
+    if (list_size) *list_size = p->list_size;
+    return PL_OK;
+}
+
+int pl_sc_decode(const pl_plan* p, const float* llr, int64_t bs, void* out, int32_t out_kind, void* stream) {
+    if (!p || bs < 0 || (bs > 0 && (!llr || (!out && p->k > 0)))) {
+        pl::set_error("pl_sc_decode: bad arguments");
+        return PL_EINVAL;
+    }
+    if (out_kind != PL_OUT_F32 && out_kind != PL_OUT_U8) {
+        pl::set_error("pl_sc_decode: unknown out_kind");
+        return PL_EINVAL;
+    }
+    return pl::launch_sc(p, llr, bs, out, out_kind, static_cast<hipStream_t>(stream));
+}
+
+size_t pl_scl_workspace_size(const pl_plan* p, int64_t bs) { return p ? pl::scl_workspace_size(p, bs) : 0; }
+
+int pl_scl_decode(const pl_plan* p, const float* llr, int64_t bs, void* out, int32_t out_kind, double* out_pm,
+                  void* ws, size_t ws_bytes, void* stream) {
+    if (!p || bs < 0 || (bs > 0 && (!llr || (!out && p->k > 0)))) {
+        pl::set_error("pl_scl_decode: bad arguments");
+        return PL_EINVAL;
+    }
+    if (out_kind != PL_OUT_F32 && out_kind != PL_OUT_U8) {
+        pl::set_error("pl_scl_decode: unknown out_kind");
+        return PL_EINVAL;
+    }
+    if (ws_bytes < pl::scl_workspace_size(p, bs)) {
+        pl::set_error("pl_scl_decode: workspace too small");
+        return PL_EINVAL;
+    }
+    return pl::launch_scl(p, llr, bs, out, out_kind, out_pm, ws, ws_bytes, static_cast<hipStream_t>(stream));
+}
+
+int pl_polar_encode(const pl_plan* p, const float* u, int64_t bs, float* cw, void* stream) {
+    if (!p || bs < 0 || (bs > 0 && (!cw || (!u && p->k > 0)))) {
+        pl::set_error("pl_polar_encode: bad arguments");
+        return PL_EINVAL;
+    }
+    return pl::launch_encode(p, u, bs, cw, static_cast<hipStream_t>(stream));
+}
+
+}  // extern "C"

@@ -1,0 +1,30 @@
+// plan.h -- internal (non-ABI) plan layout shared by the HIP translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+struct pl_plan {
+    int32_t n = 0, log_n = 0, k = 0, list_size = 1, f_mode = 0;
+    float llr_max = 30.0f;
+    uint32_t flags = 0;
+    // Device-resident, immutable after pl_plan_create:
+    uint32_t* d_frozen_words = nullptr;  // ceil(n/32) words, bit (i&31) of word i>>5 = frozen[i]
+    uint32_t* d_rate0_words = nullptr;   // n-1 node flags: bit OFF(s)+(p>>s), OFF(s)=n-(n>>(s-1))
+    int32_t* d_info_pos = nullptr;       // k ascending information positions
+    int32_t* d_info_rank = nullptr;      // n entries: rank among info positions, -1 if frozen
+};
+
+namespace pl {
+void set_error(const std::string& msg);
+int check_hip(hipError_t e, const char* what);
+
+// Launchers (return PL_* codes); defined in sc_kernel.hip / scl_kernel.hip / encode_kernel.hip
+int launch_sc(const pl_plan* plan, const float* llr, int64_t bs, void* out, int out_kind,
+              hipStream_t stream);
+size_t scl_workspace_size(const pl_plan* plan, int64_t bs);
+int launch_scl(const pl_plan* plan, const float* llr, int64_t bs, void* out, int out_kind,
+               double* out_pm, void* ws, size_t ws_bytes, hipStream_t stream);
+int launch_encode(const pl_plan* plan, const float* u, int64_t bs, float* cw, hipStream_t stream);
+}  // namespace pl

@@ -1,0 +1,87 @@
+"""Tensor-level entry points over the C ABI (device tensors in, device tensors out).
+
+Every function here launches a hand-written gfx950 kernel from libpolar_mi355x.so on the
+current torch stream of the tensor's device; nothing runs on the CPU and there is no fallback.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+
+
+def _require_cuda(t, name):
+    if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+        raise RuntimeError(f"{name} must be a tensor on a ROCm GPU (got "
+                           f"{getattr(t, 'device', type(t))}); the MI355X decoder has no CPU path")
+
+
+def _out_kind(dtype):
+    if dtype == torch.float32:
+        return _lib.PL_OUT_F32
+    if dtype == torch.uint8:
+        return _lib.PL_OUT_U8
+    raise ValueError(f"unsupported decoder output dtype {dtype}")
+
+
+def sc_decode(plan, llr_logits, out=None, out_dtype=torch.float32):
+    """SC-decode [bs, n] fp32 logits on the GPU -> [bs, k] bits (polar_sc.py:113-133 semantics)."""
+    _require_cuda(llr_logits, "llr_logits")
+    x = llr_logits
+    if x.dtype != torch.float32 or not x.is_contiguous():
+        x = x.to(torch.float32).contiguous()
+    if x.dim() != 2 or x.shape[1] != plan.n:
+        raise ValueError(f"llr_logits must be [bs, {plan.n}], got {tuple(x.shape)}")
+    bs = x.shape[0]
+    if out is None:
+        out = torch.empty((bs, plan.k), dtype=out_dtype, device=x.device)
+    elif out.shape != (bs, plan.k) or not out.is_contiguous() or out.device != x.device:
+        raise ValueError("out must be a contiguous [bs, k] tensor on the input's device")
+    kind = _out_kind(out.dtype)
+    with torch.cuda.device(x.device):
+        st = _lib.current_stream_ptr(x.device)
+        _lib.check(_lib.lib().pl_sc_decode(plan.handle, ctypes.c_void_p(x.data_ptr()), bs,
+                                           ctypes.c_void_p(out.data_ptr()), kind, st), "pl_sc_decode")
+    return out
+
+
+def scl_decode(plan, llr_logits, out=None, out_dtype=torch.float32, return_pm=False):
+    """SCL-decode [bs, n] fp32 logits -> [bs, k] bits (+ sorted path metrics [bs, 2L] fp64)."""
+    _require_cuda(llr_logits, "llr_logits")
+    x = llr_logits
+    if x.dtype != torch.float32 or not x.is_contiguous():
+        x = x.to(torch.float32).contiguous()
+    if x.dim() != 2 or x.shape[1] != plan.n:
+        raise ValueError(f"llr_logits must be [bs, {plan.n}], got {tuple(x.shape)}")
+    bs = x.shape[0]
+    if out is None:
+        out = torch.empty((bs, plan.k), dtype=out_dtype, device=x.device)
+    kind = _out_kind(out.dtype)
+    pm = torch.empty((bs, 2 * plan.list_size), dtype=torch.float64, device=x.device) if return_pm else None
+    L = _lib.lib()
+    ws_bytes = int(L.pl_scl_workspace_size(plan.handle, bs))
+    ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=x.device)
+    with torch.cuda.device(x.device):
+        st = _lib.current_stream_ptr(x.device)
+        _lib.check(L.pl_scl_decode(plan.handle, ctypes.c_void_p(x.data_ptr()), bs, ctypes.c_void_p(out.data_ptr()),
+                                   kind, ctypes.c_void_p(pm.data_ptr() if pm is not None else 0),
+                                   ctypes.c_void_p(ws.data_ptr()), ws_bytes, st), "pl_scl_decode")
+    return (out, pm) if return_pm else out
+
+
+def polar_encode(plan, u_bits, out=None):
+    """Encode [bs, k] 0/1 fp32 information bits -> [bs, n] fp32 codewords (enc.py:30-43)."""
+    _require_cuda(u_bits, "u_bits")
+    u = u_bits
+    if u.dtype != torch.float32 or not u.is_contiguous():
+        u = u.to(torch.float32).contiguous()
+    if u.dim() != 2 or u.shape[1] != plan.k:
+        raise ValueError(f"u_bits must be [bs, {plan.k}], got {tuple(u.shape)}")
+    bs = u.shape[0]
+    if out is None:
+        out = torch.empty((bs, plan.n), dtype=torch.float32, device=u.device)
+    with torch.cuda.device(u.device):
+        st = _lib.current_stream_ptr(u.device)
+        _lib.check(_lib.lib().pl_polar_encode(plan.handle, ctypes.c_void_p(u.data_ptr()), bs,
+                                              ctypes.c_void_p(out.data_ptr()), st), "pl_polar_encode")
+    return out

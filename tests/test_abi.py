@@ -1,0 +1,65 @@
+"""CPU-side checks of the C-ABI library: it loads and exports every symbol include/*.h declares.
+
+No compute calls here (there is no GPU in the build container).
+"""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "polar_mi355x.h")
+
+
+def _declared():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(pl_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_header_declares_expected_api():
+    names = _declared()
+    for must in ("pl_plan_create", "pl_plan_destroy", "pl_sc_decode", "pl_scl_decode", "pl_last_error_string"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    from polar_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.fail(f"{_lib.LIB_PATH} not built (run __graft_entry__.build())")
+    L = _lib.lib()
+    for name in _declared():
+        assert hasattr(L, name), f"{name} declared in include/polar_mi355x.h but not exported"
+    assert set(_lib.EXPORTED_SYMBOLS) == set(_declared())
+    assert L.pl_version().decode().startswith("polar_mi355x")
+
+
+def test_library_targets_gfx950():
+    from polar_amd import _lib
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_plan_create_rejects_bad_arguments_without_gpu():
+    # argument validation happens before any HIP call, so it is testable on the CPU
+    import numpy as np
+    from polar_amd import _lib
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    mask = np.zeros(6, dtype=np.uint8)
+    assert L.pl_plan_create(ctypes.byref(h), 6, mask.ctypes.data_as(ctypes.c_void_p), 1, 0, 30.0, 0) == _lib.PL_EINVAL
+    assert b"power of two" in L.pl_last_error_string()
+    mask = np.zeros(8, dtype=np.uint8)
+    assert L.pl_plan_create(ctypes.byref(h), 8, mask.ctypes.data_as(ctypes.c_void_p), 3, 0, 30.0, 0) == _lib.PL_EINVAL
+    assert L.pl_plan_create(ctypes.byref(h), 8, mask.ctypes.data_as(ctypes.c_void_p), 1, 7, 30.0, 0) == _lib.PL_EINVAL
+
+
+def test_no_cpu_fallback_without_gpu():
+    import torch
+    import polar_amd
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    dec = polar_amd.SC_Dec(torch.arange(32), 64)
+    with pytest.raises(RuntimeError):
+        dec(torch.zeros(2, 64))

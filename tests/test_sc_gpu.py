@@ -1,0 +1,148 @@
+"""Parity of the HIP SC decoder (libpolar_mi355x.so via the C ABI) with the reference.
+
+  * golden fixtures from the reference (tests/golden/sc_*.npz): bit-exact, min-sum
+  * the pinned CPU oracle on seeded random inputs, every supported n: bit-exact
+  * full-size (512,1024) x 65536 batch: noiseless encode->decode round trip + oracle on a sample
+  * edge cases: bs = 0 / 1 / ragged, k = 0 / n, exact zeros, saturation, uint8 output, CPU input
+  * exact-boxplus mode: statistical gate (see tests/test_oracle.py for why)
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def pa():
+    import polar_amd
+    assert torch.cuda.is_available(), "GPU tests need a ROCm GPU"
+    return polar_amd
+
+
+def _plan(pa, fp, n, f_mode=0, L=1):
+    from polar_amd import _lib
+    return _lib.Plan(n, pa.frozen_mask(fp, n), L, f_mode)
+
+
+def _sets(d):
+    return [k[4:] for k in d.files if k.startswith("llr_")]
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "sc_*.npz"))), ids=os.path.basename)
+def test_sc_golden_bit_exact(pa, path):
+    d = np.load(path)
+    n = int(d["n"])
+    plan = _plan(pa, d["frozen_pos"], n)
+    for name in _sets(d):
+        x = torch.from_numpy(d["llr_" + name]).cuda()
+        bits = pa.ops.sc_decode(plan, x)
+        torch.cuda.synchronize()
+        got = bits.cpu().numpy().astype(np.uint8)
+        assert np.array_equal(got, d["bits_" + name]), f"{name}: {int((got != d['bits_' + name]).any(1).sum())} rows differ"
+
+
+@pytest.mark.parametrize("log_n", list(range(1, 12)))
+@pytest.mark.parametrize("rate", [0.25, 0.5, 0.75])
+def test_sc_random_vs_oracle(pa, log_n, rate):
+    n = 1 << log_n
+    rng = np.random.default_rng(log_n * 10 + int(rate * 4))
+    k = max(1, int(n * rate))
+    fp = np.sort(rng.permutation(n)[: n - k])  # arbitrary frozen set: exercises all node patterns
+    bs = 300 + log_n  # ragged: not a multiple of the per-block codeword count
+    llr = (rng.standard_normal((bs, n)) * 3).astype(np.float32)
+    llr[rng.random((bs, n)) < 0.05] = 0.0
+    want = oracle.sc_decode(llr, fp)
+    plan = _plan(pa, fp, n)
+    got = pa.ops.sc_decode(plan, torch.from_numpy(llr).cuda()).cpu().numpy()
+    assert np.array_equal(got, want)
+    got8 = pa.ops.sc_decode(plan, torch.from_numpy(llr).cuda(), out_dtype=torch.uint8).cpu().numpy()
+    assert np.array_equal(got8, want.astype(np.uint8))
+
+
+def test_sc_reference_frozen_all_shapes(pa):
+    fs = np.load(os.path.join(GOLDEN, "frozen_sets.npz"))
+    rng = np.random.default_rng(5)
+    for key in fs.files:
+        k, n = (int(v[1:]) for v in key.split("_"))
+        if n > 2048:
+            continue
+        fp = fs[key]
+        llr = (rng.standard_normal((129, n)) * 2 + 0.5).astype(np.float32)
+        got = pa.ops.sc_decode(_plan(pa, fp, n), torch.from_numpy(llr).cuda()).cpu().numpy()
+        assert np.array_equal(got, oracle.sc_decode(llr, fp)), key
+
+
+def test_sc_full_batch_roundtrip_and_sample(pa):
+    """(512,1024) at the bench batch: size-independent property + oracle on a sample."""
+    fp = pa.reference_frozen_pos(512, 1024).numpy()
+    plan = _plan(pa, fp, 1024)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    bs = 65536
+    u = torch.randint(0, 2, (bs, 512), device="cuda", generator=g).to(torch.float32)
+    cw = pa.ops.polar_encode(plan, u)
+    logits = (2.0 * cw - 1.0) * 3.0  # noiseless: logits > 0 <=> bit 1
+    assert torch.equal(pa.ops.sc_decode(plan, logits), u)
+    noisy = logits + torch.randn(logits.shape, device="cuda", generator=g) * 2.0
+    got = pa.ops.sc_decode(plan, noisy)
+    idx = torch.randint(0, bs, (512,), device="cuda", generator=g)
+    sample = noisy[idx].cpu().numpy()
+    assert np.array_equal(got[idx].cpu().numpy(), oracle.sc_decode(sample, fp))
+
+
+def test_sc_edge_cases(pa):
+    n = 64
+    fp = pa.reference_frozen_pos(32, 64).numpy()
+    plan = _plan(pa, fp, n)
+    empty = pa.ops.sc_decode(plan, torch.empty((0, n), device="cuda"))
+    assert empty.shape == (0, 32)
+    one = (torch.randn(1, n) * 2).cuda()
+    assert np.array_equal(pa.ops.sc_decode(plan, one).cpu().numpy(), oracle.sc_decode(one.cpu().numpy(), fp))
+    # all frozen (k = 0) and nothing frozen (k = n)
+    p0 = _plan(pa, np.arange(n), n)
+    assert pa.ops.sc_decode(p0, one).shape == (1, 0)
+    pn = _plan(pa, np.array([], dtype=np.int64), n)
+    x = (torch.randn(77, n) * 2)
+    x[:, ::7] = 0.0
+    assert np.array_equal(pa.ops.sc_decode(pn, x.cuda()).cpu().numpy(), oracle.sc_decode(x.numpy(), []))
+    # saturation far beyond the +-30 clip and signed zeros
+    y = (torch.randn(200, n) * 500)
+    y[:, 3] = -0.0
+    assert np.array_equal(pa.ops.sc_decode(plan, y.cuda()).cpu().numpy(), oracle.sc_decode(y.numpy(), fp))
+    with pytest.raises(ValueError):
+        pa.ops.sc_decode(plan, torch.zeros((4, n + 1), device="cuda"))
+
+
+def test_sc_dropin_module_matches_reference_contract(pa):
+    d = np.load(os.path.join(GOLDEN, "sc_32_64.npz"))
+    fp = torch.from_numpy(d["frozen_pos"].astype(np.int64))
+    dec = pa.SC_Dec(fp, 64)
+    x = torch.from_numpy(d["llr_rand"])  # CPU tensor, as the reference harness passes
+    out = dec(x)
+    assert out.device.type == "cpu" and out.dtype == torch.float32 and out.shape == (x.shape[0], 32)
+    assert np.array_equal(out.numpy().astype(np.uint8), d["bits_rand"])
+    out3 = dec(x.reshape(4, -1, 64))  # [..., n] input -> [-1, ..., k] output (polar_sc.py:129-132)
+    assert out3.shape == (4, x.shape[0] // 4, 32)
+    with pytest.raises(AssertionError):
+        dec(torch.zeros(64))
+    with pytest.raises(AssertionError):
+        dec(torch.zeros(3, 63))
+    assert dec(x.cuda()).device.type == "cuda"
+
+
+def test_sc_exact_mode_statistical(pa):
+    for path in sorted(glob.glob(os.path.join(GOLDEN, "sc_*.npz"))):
+        d = np.load(path)
+        plan = _plan(pa, d["frozen_pos"], int(d["n"]), f_mode=1)
+        for name in _sets(d):
+            if not name.startswith("awgn"):
+                continue
+            got = pa.ops.sc_decode(plan, torch.from_numpy(d["llr_" + name]).cuda()).cpu().numpy().astype(np.uint8)
+            rate = float((got != d["exact_" + name]).any(1).mean())
+            assert rate <= 0.02, (path, name, rate)
