@@ -1,0 +1,192 @@
+"""bench.py -- SC decode throughput on MI355X (BASELINE.json metric), 1..8 GPUs, one process per GPU.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Workload (BASELINE.json configs[2], and per GPU of configs[4]): SC decoding of (k=512, n=1024) polar
+codewords, bs=65536 per GPU, AWGN LLRs at Eb/N0 = 2 dB (synthetic, generated on device with the
+port of System_AWGN_model, seed 42+rank).  A step = one decode launch over the resident batch.
+Weak scaling: each rank decodes its own 65536 codewords (no data-path collective); ranks only
+all_reduce the block-error counters (BLER) and the timing.
+
+Reported: value = codewords decoded by all ranks / max-over-ranks wall time (Mcodewords/s);
+roofline = algorithmic HBM bytes per launch (bs*(4n+4k): fp32 LLRs in, fp32 bits out) / average
+launch time from HIP events on the decode stream, against 8.0 TB/s; cpu_baseline = the C oracle
+(same algorithm, OpenMP) on host cores, rank 0 at N=1 only, bounded to ~10 s.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "polar-code-pytorch-sionna_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "Mcodewords/s + info-bit Gbit/s, SC n=1024 bs=65536 @1/2/4/8 GPU; BLER match"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md, chip-level parameters (spec)
+REF_BLER_2DB = 0.9999  # reference x_run SC BLER at (512,1024), 2.0 dB
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--k", type=int, default=512)
+    ap.add_argument("--n", type=int, default=1024)
+    ap.add_argument("--bs", type=int, default=65536, help="codewords per GPU")
+    ap.add_argument("--ebno", type=float, default=2.0)
+    ap.add_argument("--decoder", choices=["sc", "scl"], default="sc")
+    ap.add_argument("--list-size", type=int, default=8)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(llr_host, fp, k, n, decoder, L, budget_s):
+    """The pinned C oracle (port of the reference algorithm) on the host cores, bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    oracle.build()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
+    if decoder == "sc":
+        sample = llr_host[: min(len(llr_host), 65536)]
+        fn = lambda x: oracle.sc_decode(x, fp, nthreads=threads)  # noqa: E731
+    else:
+        sample = llr_host[: min(len(llr_host), 4 * threads)]
+        fn = lambda x: oracle.scl_decode(x, fp, L, nthreads=threads, lazy=True)  # noqa: E731
+    fn(sample[: min(len(sample), 256)])  # warm the thread pool
+    done, t0 = 0, time.perf_counter()
+    while True:
+        fn(sample)
+        done += len(sample)
+        if time.perf_counter() - t0 >= budget_s or done >= 64 * len(sample):
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(done / dt / 1e6, 6), "unit": "Mcodewords/s", "cores": threads, "kind": "port",
+            "sample": f"{done} codewords ({len(sample)}-codeword batches of the same AWGN LLRs, "
+                      f"(k={k},n={n}) {decoder.upper()}, oracle/polar_oracle.c OpenMP) in {dt:.1f} s",
+            "reference_cpu_note": "reference x_run SC_Dec measured in the build container (8 Xeon "
+                                  "threads): 0.00603 Mcodewords/s at this shape (BASELINE.md §2)"}
+
+
+def traffic_from_profiles(tag):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if one exists for this shape."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        return json.load(open(path)).get(tag, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import polar_amd
+    from polar_amd import _lib, channel, ops
+
+    k, n, bs = a.k, a.n, a.bs
+    fp = polar_amd.reference_frozen_pos(k, n)
+    mask = polar_amd.frozen_mask(fp, n)
+    L = a.list_size if a.decoder == "scl" else 1
+    plan = _lib.Plan(n, mask, L, _lib.PL_F_MINSUM)
+    gen = torch.Generator(device=dev).manual_seed(42 + rank)
+    model = channel.System_AWGN_model(n, k, channel.GpuEncoder(fp, n), None, device=dev, generator=gen)
+    with torch.no_grad():
+        bits, _, llr = model.llrs(bs, torch.tensor(a.ebno, dtype=torch.float32))
+    llr = llr.contiguous()
+    out = torch.empty((bs, k), dtype=torch.float32, device=dev)
+    ws = None
+    if a.decoder == "scl":
+        ws_bytes = int(_lib.lib().pl_scl_workspace_size(plan.handle, bs))
+        ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=dev)
+
+    def step():
+        if a.decoder == "sc":
+            ops.sc_decode(plan, llr, out=out)
+        else:
+            ops.scl_decode(plan, llr, out=out)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    stream = torch.cuda.current_stream(dev)  # the decode kernels launch on this stream
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(a.steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    kern_ms = e0.elapsed_time(e1) / a.steps
+
+    blk = torch.tensor([int(torch.any(out != bits, dim=-1).sum().item()), bs], dtype=torch.int64, device=dev)
+    tmax = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(blk, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    wall = float(tmax.item())
+    total_cw = bs * world * a.steps
+    value = total_cw / wall / 1e6
+    bytes_per_launch = bs * (4 * n + 4 * k)
+    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+    tag = f"{a.decoder}_k{k}_n{n}_bs{bs}" + (f"_L{L}" if L > 1 else "")
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(llr.cpu().numpy(), fp.numpy(), k, n, a.decoder, L, a.cpu_seconds)
+    if rank == 0:
+        line = {
+            "metric": METRIC if a.decoder == "sc" else f"Mcodewords/s, SCL L={L} n={n}",
+            "value": round(value, 4),
+            "unit": "Mcodewords/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(wall / a.steps * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": f"synthetic AWGN LLRs, Eb/N0={a.ebno} dB, QPSK, generated on device (seed 42+rank)",
+            "config": {"workload": f"{a.decoder.upper()} decode (k={k}, n={n}), bs={bs} per GPU"
+                                   + (f", L={L}" if L > 1 else ""),
+                       "k": k, "n": n, "bs_per_gpu": bs, "global_batch": bs * world,
+                       "parallelism": f"dp{world}"},
+            "info_gbit_s": round(total_cw * k / wall / 1e9, 4),
+            "bler": round(float(blk[0].item()) / float(blk[1].item()), 6),
+            "bler_reference_at_ebno": REF_BLER_2DB if (a.decoder == "sc" and k == 512 and n == 1024 and a.ebno == 2.0) else None,
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic_from_profiles(tag),
+                         "kernel_ms": round(kern_ms, 5), "algorithmic_bytes_per_launch": bytes_per_launch},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,188 @@
+"""LLR producer for the decoder: bits -> polar encoder -> QPSK -> AWGN -> logits (any torch device).
+
+Numerically this follows the reference blocks op for op, in the same RNG call order, so that on
+the CPU device it reproduces the reference's LLRs bit for bit (pinned by tests/golden/harness_c1.npz):
+  ebnodb2no        my_sn/trans/ebno.py:2-24
+  BinarySource     my_sn/trans/binary_source.py:14-19           (randint, float32)
+  QamConstell      my_sn/trans/mapping.py:7-48, :49-95          (Gray QPSK, unit energy)
+  Mapper           my_sn/trans/mapping.py:97-149
+  AWGN             my_sn/trans/channel/awgn.py:6-29 + my_sn/utils.py:2-17 (two torch.normal draws)
+  Demapper         my_sn/trans/mapping.py:151-241              (logsumexp, logits log P1/P0)
+  System_AWGN_model  x_run_sn_polar/z_sys_model/awgn_model.py:17-44
+On a GPU the same ops run on device (different RNG stream, same distribution) and the encoder is
+the HIP XOR-butterfly kernel (bit-identical to the reference's dense c@G % 2, enc.py:42).
+"""
+import numpy as np
+import torch as tc
+from torch import nn
+
+
+def ebnodb2no(ebno_db, n_bits_per_sym, coderate):
+    ebno = 10. ** (ebno_db / 10.)
+    return 1 / (ebno * coderate * n_bits_per_sym / 1)
+
+
+def _qam_points(n_bits_per_sym):
+    """Gray-labelled, unit-energy QAM points as complex64 numpy (mapping.py:7-48 arithmetic)."""
+    assert n_bits_per_sym % 2 == 0 and n_bits_per_sym > 0
+
+    def pam(b):
+        if len(b) > 1:
+            return (1 - 2 * b[0]) * (2 ** len(b[1:]) - pam(b[1:]))
+        return 1 - 2 * b[0]
+
+    c = np.zeros([2 ** n_bits_per_sym], dtype=np.complex64)
+    for i in range(2 ** n_bits_per_sym):
+        b = np.array(list(np.binary_repr(i, n_bits_per_sym)), dtype=np.int16)
+        c[i] = pam(b[0::2]) + 1j * pam(b[1::2])
+    m = n_bits_per_sym // 2
+    var = 1 / (2 ** (m - 2)) * np.sum(np.linspace(1, 2 ** m - 1, 2 ** (m - 1)) ** 2)
+    c /= np.sqrt(var)
+    return c
+
+
+class QamConstellation(nn.Module):
+    def __init__(self, n_bits_per_symbol=2, device='cpu'):
+        super().__init__()
+        self.n_bits_per_sym = int(n_bits_per_symbol)
+        self.dtype = tc.complex64
+        self.device = device
+        p = tc.from_numpy(_qam_points(self.n_bits_per_sym)).to(dtype=tc.complex64, device=device)
+        self._points = tc.stack([tc.real(p), tc.imag(p)], dim=0).to(tc.float32)
+
+    @property
+    def points(self):
+        x = tc.complex(self._points[0], self._points[1])
+        energy = tc.mean(tc.abs(x) ** 2)
+        return x / tc.sqrt(energy).to(dtype=self.dtype)
+
+
+class BinarySource(nn.Module):
+    def __init__(self, dtype=tc.float32, device='cpu', generator=None):
+        super().__init__()
+        self.dtype, self.device, self.generator = dtype, device, generator
+
+    def forward(self, shape):
+        return tc.randint(0, 2, size=shape, device=self.device, dtype=self.dtype, generator=self.generator)
+
+
+class Mapper(nn.Module):
+    def __init__(self, constell):
+        super().__init__()
+        self.constell = constell
+        m = constell.n_bits_per_sym
+        self._base = 2 ** tc.tensor(range(m - 1, -1, -1), device=constell.device)
+
+    def forward(self, bits):
+        m = self.constell.n_bits_per_sym
+        shape = [-1] + list(bits.shape[1:-1]) + [int(bits.shape[-1] / m), m]
+        idx = tc.sum(bits.reshape(shape).to(tc.int32) * self._base, dim=-1)
+        return self.constell.points[idx]
+
+
+class AWGN(nn.Module):
+    def __init__(self, device='cpu', generator=None):
+        super().__init__()
+        self.device, self.generator = device, generator
+
+    def forward(self, inputs):
+        x, no = inputs
+        # utils.py:11-15 passes a 0-dim fp32 tensor; the arg parser reads it as this same double
+        std = float(tc.sqrt(tc.tensor(1.0 / 2, dtype=tc.float32)))
+        kw = dict(size=x.shape, dtype=tc.float32, device=self.device)
+        if self.generator is not None:
+            kw["generator"] = self.generator
+        xr = tc.normal(mean=0, std=std, **kw)
+        xi = tc.normal(mean=0, std=std, **kw)
+        noise = tc.complex(xr, xi)
+        no = tc.as_tensor(no).reshape([1] * len(x.shape)) if tc.is_tensor(no) and no.dim() == 0 else no
+        noise *= tc.sqrt(tc.as_tensor(no).to(dtype=tc.float32)).to(dtype=noise.dtype, device=self.device)
+        return x + noise
+
+
+class Demapper(nn.Module):
+    """Exact (logsumexp) demapper: logits log(P(b=1)/P(b=0)) per bit."""
+
+    def __init__(self, constell):
+        super().__init__()
+        self.constell = constell
+        m = constell.n_bits_per_sym
+        npts = 2 ** m
+        a = np.array([list(np.binary_repr(i, m)) for i in range(npts)], dtype=np.int16)
+        c0 = np.stack([np.where(a[:, i] == 0)[0] for i in range(m)], axis=1)
+        c1 = np.stack([np.where(a[:, i] == 1)[0] for i in range(m)], axis=1)
+        self._c0 = tc.tensor(c0, dtype=tc.int64)
+        self._c1 = tc.tensor(c1, dtype=tc.int64)
+
+    def forward(self, inputs):
+        y, no = inputs
+        pts = self.constell.points.reshape([1] * len(y.shape) + [-1])
+        sq = tc.abs(y.unsqueeze(dim=-1) - pts) ** 2
+        no_t = tc.as_tensor(no)
+        no_t = no_t.reshape(list(no_t.shape) + [1] * (len(sq.shape) - no_t.dim())).to(y.device)
+        e = -sq / no_t
+        llr = tc.logsumexp(e[..., self._c1.to(e.device)], dim=-2) - tc.logsumexp(e[..., self._c0.to(e.device)], dim=-2)
+        return llr.reshape(list(y.shape[:-1]) + [y.shape[-1] * self.constell.n_bits_per_sym])
+
+
+class DenseEncoder(nn.Module):
+    """c[:, info_pos] = u; (c @ G) % 2 -- the reference harness encoder (enc.py:30-43), any device."""
+
+    def __init__(self, frozen_pos, n, G, device='cpu'):
+        super().__init__()
+        fp = frozen_pos.cpu().numpy() if tc.is_tensor(frozen_pos) else np.asarray(frozen_pos)
+        self.n = n
+        self.info_pos = tc.from_numpy(np.setdiff1d(np.arange(n), fp)).to(device)
+        self.G = G.to(device)
+
+    def forward(self, u):
+        c = tc.zeros([u.shape[0], self.n], dtype=tc.float32, device=u.device)
+        c[..., self.info_pos] = u
+        return (c @ self.G % 2).to(tc.float32)
+
+
+class GpuEncoder(nn.Module):
+    """Polar encoder on the GPU through the HIP butterfly kernel (same output as DenseEncoder)."""
+
+    def __init__(self, frozen_pos, n):
+        super().__init__()
+        from . import _lib
+        from .frozen import frozen_mask
+        self._plan = _lib.Plan(n, frozen_mask(frozen_pos, n), 1)
+
+    def forward(self, u):
+        from . import ops
+        return ops.polar_encode(self._plan, u)
+
+
+class System_AWGN_model(nn.Module):
+    """bits -> encoder -> QPSK -> AWGN -> demapper -> decoder (awgn_model.py:17-44)."""
+
+    def __init__(self, n, k, encoder, decoder, cw_estimates=False, device='cpu', generator=None):
+        super().__init__()
+        self.cw_estimates = cw_estimates
+        self.n_bits_per_sym = 2
+        self.n, self.k = n, k
+        self.coderate = self.k / self.n
+        self.constell = QamConstellation(self.n_bits_per_sym, device=device)
+        self.mapper = Mapper(self.constell)
+        self.demapper = Demapper(self.constell)
+        self.binary_src = BinarySource(device=device, generator=generator)
+        self.awgn_channel = AWGN(device=device, generator=generator)
+        self.encoder, self.decoder = encoder, decoder
+
+    def llrs(self, batch_size, ebno_db):
+        """The channel half of forward(): (bits, codewords, logits)."""
+        no = ebnodb2no(ebno_db, self.n_bits_per_sym, self.coderate)
+        bits = self.binary_src([batch_size, self.k])
+        codewords = self.encoder(bits)
+        x = self.mapper(codewords)
+        y = self.awgn_channel([x, no])
+        return bits, codewords, self.demapper([y, no])
+
+    def forward(self, batch_size, ebno_db):
+        bits, codewords, llr = self.llrs(batch_size, ebno_db)
+        bits_hat = self.decoder(llr)
+        if self.cw_estimates:
+            return codewords, bits_hat
+        return bits, bits_hat

@@ -1,0 +1,114 @@
+"""Parity of the HIP SC-list decoder with the reference (x_run_sn_polar/polar/polar_scl.py).
+
+Bits must be identical; path metrics (the reference's final sorted msg_pm, float64) within 1e-9
+absolute (BASELINE.json asks 1e-5): the kernel keeps LLRs and metrics in fp64 like the reference,
+so only exp/log last-ulp differences remain.  On inputs that create exact path-metric ties the
+reference's own order is host-dependent (unstable np.argsort); there the decoder is held to the
+reference re-run with a stable argsort (tests/golden/make_golden.py).
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+NO_TIE_SETS = ("rand", "awgn0", "awgn2", "awgn4")
+PM_TOL = 1e-9
+
+
+@pytest.fixture(scope="module")
+def pa():
+    import polar_amd
+    assert torch.cuda.is_available()
+    return polar_amd
+
+
+def _plan(pa, fp, n, L):
+    from polar_amd import _lib
+    return _lib.Plan(n, pa.frozen_mask(fp, n), L, 0)
+
+
+def _sets(d):
+    return [k[4:] for k in d.files if k.startswith("llr_")]
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "scl_*.npz"))), ids=os.path.basename)
+def test_scl_golden(pa, path):
+    d = np.load(path)
+    n, L = int(d["n"]), int(d["L"])
+    plan = _plan(pa, d["frozen_pos"], n, L)
+    for name in _sets(d):
+        bits, pm = pa.ops.scl_decode(plan, torch.from_numpy(d["llr_" + name]).cuda(), return_pm=True)
+        bits = bits.cpu().numpy().astype(np.uint8)
+        pm = pm.cpu().numpy()
+        assert np.array_equal(bits, d["bits_stable_" + name]), name
+        assert np.abs(pm - d["pm_stable_" + name]).max() <= PM_TOL, name
+        if name in NO_TIE_SETS:
+            assert np.array_equal(bits, d["bits_" + name]), name
+            assert np.abs(pm - d["pm_" + name]).max() <= PM_TOL, name
+
+
+@pytest.mark.parametrize("log_n", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
+@pytest.mark.parametrize("L", [1, 2, 8, 32])
+def test_scl_random_vs_oracle(pa, log_n, L):
+    n = 1 << log_n
+    if n * L > 32768 or (log_n >= 9 and L == 32):
+        pytest.skip("oracle runtime")
+    rng = np.random.default_rng(log_n * 100 + L)
+    k = max(1, n // 2)
+    fp = np.sort(rng.permutation(n)[: n - k])
+    bs = 67 if n >= 512 else 131
+    llr = (rng.standard_normal((bs, n)) * 2.5 + 0.7).astype(np.float32)
+    want_b, want_pm = oracle.scl_decode(llr, fp, L, lazy=True)
+    bits, pm = pa.ops.scl_decode(_plan(pa, fp, n, L), torch.from_numpy(llr).cuda(), return_pm=True)
+    assert np.array_equal(bits.cpu().numpy(), want_b)
+    assert np.abs(pm.cpu().numpy() - want_pm).max() <= PM_TOL
+
+
+def test_scl_bench_shape_sample(pa):
+    """(512,1024), L=8 at the bench batch (8192): oracle on a sample + noiseless round trip."""
+    fp = pa.reference_frozen_pos(512, 1024).numpy()
+    plan = _plan(pa, fp, 1024, 8)
+    g = torch.Generator(device="cuda").manual_seed(11)
+    u = torch.randint(0, 2, (8192, 512), device="cuda", generator=g).to(torch.float32)
+    enc = _plan(pa, fp, 1024, 1)
+    cw = pa.ops.polar_encode(enc, u)
+    logits = (2.0 * cw - 1.0) * 2.0 + torch.randn(cw.shape, device="cuda", generator=g) * 1.2
+    bits = pa.ops.scl_decode(plan, logits)
+    idx = torch.arange(0, 8192, 8192 // 24, device="cuda")
+    want, _ = oracle.scl_decode(logits[idx].cpu().numpy(), fp, 8, lazy=True)
+    assert np.array_equal(bits[idx].cpu().numpy(), want)
+    clean = pa.ops.scl_decode(plan, (2.0 * cw - 1.0) * 3.0)
+    assert torch.equal(clean, u)
+
+
+def test_scl_edge_cases(pa):
+    fp = pa.reference_frozen_pos(32, 64).numpy()
+    plan = _plan(pa, fp, 64, 8)
+    assert pa.ops.scl_decode(plan, torch.empty((0, 64), device="cuda")).shape == (0, 32)
+    x = torch.randn(5, 64) * 2
+    b, pm = pa.ops.scl_decode(_plan(pa, np.arange(64), 64, 4), x.cuda(), return_pm=True)  # k = 0
+    wb, wpm = oracle.scl_decode(x.numpy(), np.arange(64), 4)
+    assert b.shape == (5, 0) and np.abs(pm.cpu().numpy() - wpm).max() <= PM_TOL
+    b, pm = pa.ops.scl_decode(_plan(pa, [], 64, 4), x.cuda(), return_pm=True)  # k = n
+    wb, wpm = oracle.scl_decode(x.numpy(), [], 4)
+    assert np.array_equal(b.cpu().numpy(), wb) and np.abs(pm.cpu().numpy() - wpm).max() <= PM_TOL
+
+
+def test_scl_dropin_module(pa):
+    d = np.load(os.path.join(GOLDEN, "scl_L8_32_64.npz"))
+    dec = pa.SCL_Dec(torch.from_numpy(d["frozen_pos"].astype(np.int64)), 64, list_size=8)
+    x = torch.from_numpy(d["llr_rand"])
+    out = dec(x)
+    assert out.device.type == "cpu" and out.dtype == torch.float32
+    assert np.array_equal(out.numpy().astype(np.uint8), d["bits_rand"])
+    assert np.abs(dec.msg_pm - d["pm_rand"]).max() <= PM_TOL
+    with pytest.raises(AssertionError):
+        dec(x.to(torch.float64))  # polar_scl.py:213 asserts the input dtype
+    with pytest.raises(ValueError):
+        pa.SCL_Dec(d["frozen_pos"], 64, output_dtype=torch.int32)
