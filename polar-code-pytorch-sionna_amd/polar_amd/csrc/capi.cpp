@@ -48,6 +48,7 @@ void free_plan(pl_plan* p) {
     if (!p) return;
     (void)hipFree(p->d_frozen_words);
     (void)hipFree(p->d_rate0_words);
+    (void)hipFree(p->d_type_words);
     (void)hipFree(p->d_info_pos);
     (void)hipFree(p->d_info_rank);
     delete p;
@@ -104,19 +105,35 @@ int pl_plan_create(pl_plan** out, int32_t n, const uint8_t* frozen_mask, int32_t
         }
     }
     p->k = (int32_t)info.size();
-    // rate-0 flags: stage s (1..log_n-... all stages), node q = p >> s -> bit OFF(s) + q,
-    // OFF(s) = n - (n >> (s-1)).  Node is rate-0 iff every position in [q*2^s, (q+1)*2^s) is frozen.
-    std::vector<uint32_t> r0(((n - 1) + 31) / 32 + 1, 0u);
+    // Node classification (exact SC shortcuts, see sc_kernel.hip): stage s in 1..log_n, node q
+    // (positions [q*2^s, (q+1)*2^s)) -> bit OFF(s) + q with OFF(s) = n - (n >> (s-1)).
+    //   rate-0: all frozen   rate-1: none frozen   repetition: all frozen but the last
+    //   SPC: only the first frozen
+    const int nflag = n - 1;
+    const int fwords = (nflag + 31) / 32;
+    p->type_stride = fwords > 64 ? fwords : 64;
+    std::vector<uint32_t> r0(fwords + 1, 0u), types(4 * (size_t)p->type_stride, 0u);
     for (int s = 1; s <= log_n; ++s) {
         const int off = n - (n >> (s - 1));
         for (int q = 0; q < (n >> s); ++q) {
-            bool all = true;
-            for (int i = q << s; i < ((q + 1) << s) && all; ++i) all = frozen_mask[i] != 0;
-            if (all) r0[(off + q) >> 5] |= 1u << ((off + q) & 31);
+            const int a = q << s, m = 1 << s;
+            int nfz = 0;
+            for (int i = a; i < a + m; ++i) nfz += frozen_mask[i] != 0;
+            const bool is_r0 = nfz == m, is_r1 = nfz == 0;
+            const bool is_rep = nfz == m - 1 && !frozen_mask[a + m - 1];
+            const bool is_spc = nfz == 1 && frozen_mask[a];
+            const int bit = off + q;
+            const uint32_t mbit = 1u << (bit & 31);
+            if (is_r0) r0[bit >> 5] |= mbit;
+            if (is_r0) types[0 * p->type_stride + (bit >> 5)] |= mbit;
+            if (is_r1) types[1 * p->type_stride + (bit >> 5)] |= mbit;
+            if (is_rep) types[2 * p->type_stride + (bit >> 5)] |= mbit;
+            if (is_spc) types[3 * p->type_stride + (bit >> 5)] |= mbit;
         }
     }
     int r = upload(&p->d_frozen_words, fw);
     if (!r) r = upload(&p->d_rate0_words, r0);
+    if (!r) r = upload(&p->d_type_words, types);
     if (!r) r = upload(&p->d_info_rank, rank);
     if (!r && !info.empty()) r = upload(&p->d_info_pos, info);
     if (r) {

@@ -12,6 +12,8 @@ struct pl_plan {
     // Device-resident, immutable after pl_plan_create:
     uint32_t* d_frozen_words = nullptr;  // ceil(n/32) words, bit (i&31) of word i>>5 = frozen[i]
     uint32_t* d_rate0_words = nullptr;   // n-1 node flags: bit OFF(s)+(p>>s), OFF(s)=n-(n>>(s-1))
+    uint32_t* d_type_words = nullptr;    // 4 x type_stride words: rate-0 / rate-1 / repetition / SPC
+    int32_t type_stride = 64;            //   node flags, same bit indexing as d_rate0_words
     int32_t* d_info_pos = nullptr;       // k ascending information positions
     int32_t* d_info_rank = nullptr;      // n entries: rank among info positions, -1 if frozen
 };
