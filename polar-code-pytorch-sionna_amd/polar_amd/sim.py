@@ -35,7 +35,7 @@ def _row(cells, end):
 
 def sim_ber(mc_fun, ebno_dbs, batch_size, max_mc_iter, soft_estimates=False, target_bit_errs=None,
             target_block_errs=None, early_stop=True, verbose=True, dtype=tc.complex64, device='cpu',
-            process_group=None):
+            process_group=None, return_counts=False):
     """Returns (ber, bler) float tensors per SNR point, like my_sn/sim.py:sim_ber.
 
     With process_group set, each rank simulates its own batch_size codewords per iteration and the
@@ -95,6 +95,8 @@ def sim_ber(mc_fun, ebno_dbs, batch_size, max_mc_iter, soft_estimates=False, tar
     bler = c[:, 1] / c[:, 3]
     ber = tc.where(tc.isnan(ber), tc.zeros_like(ber), ber)
     bler = tc.where(tc.isnan(bler), tc.zeros_like(bler), bler)
+    if return_counts:
+        return ber, bler, c
     return ber, bler
 
 
