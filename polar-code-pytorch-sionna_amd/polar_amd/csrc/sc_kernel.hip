@@ -64,6 +64,12 @@ constexpr int kShortcuts = PL_SC_SHORTCUTS;
 #define PL_SC_ROOT_CHUNK 8  // root f/g outputs per scheduling chunk (bounds loads in flight)
 #endif
 constexpr int kWavesPerBlock = 4;
+#ifndef PL_SC_DIAG_SAMEROW
+#define PL_SC_DIAG_SAMEROW 0  // diagnostic builds only (tools/variants.py)
+#endif
+#ifndef PL_SC_DIAG_NOSTORE
+#define PL_SC_DIAG_NOSTORE 0
+#endif
 #ifndef PL_SC_LOOP_DEPTH
 #define PL_SC_LOOP_DEPTH 3  // nodes with >= 2^depth elements per lane run their children in a loop
 #endif
@@ -610,7 +616,11 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, PL_SC_MIN_WAVES) void sc_decod
     const int grp = lane >> LOG_G;
     const int64_t cw0 = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * C;
     const int64_t cw = cw0 + grp;
+#if PL_SC_DIAG_SAMEROW
+    const float* ch = llr + (size_t)((cw < bs ? cw : bs - 1) & 255) * N;  // diagnostic: L2-resident input
+#else
     const float* ch = llr + (size_t)(cw < bs ? cw : bs - 1) * N;
+#endif
 
     Ctx c;
     c.vfrozen = lane < WPC ? frozen_words[lane] : 0u;
@@ -635,6 +645,10 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, PL_SC_MIN_WAVES) void sc_decod
     }
     __syncthreads();
 
+#if PL_SC_DIAG_NOSTORE
+    if (lo == 0x123456789ull && hi == 7) static_cast<float*>(out)[cw] = 1.0f;  // diagnostic: keep the tree live
+    return;
+#endif
     // Gather the k information bits (info_pos ascending, polar_sc.py:127) -> coalesced rows.
     const uint32_t* ubase = ulds + wave * 64 * WPL;
     for (int g = 0; g < C; ++g) {

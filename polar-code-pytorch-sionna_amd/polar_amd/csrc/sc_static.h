@@ -1,0 +1,445 @@
+// sc_static.h -- code-specialised SC polar decoder kernel for gfx950 (MI355X).
+//
+// This header is compiled once per frozen set: at plan time through hiprtc (jit.cpp), or
+// ahead of time for the codes build.py pre-compiles.  The code is described by a struct
+//   struct PlCode { static constexpr int LOG_N = ..; static constexpr int FM = ..;
+//                   static constexpr unsigned char NT[2 * N] = {..}; };
+// where NT is the node-type table in heap order (node of size 2^s at position p has index
+// (N >> s) + (p >> s)); types R0/R1/REP/SPC/GEN as classified by capi.cpp.  Every branch on a
+// node type is therefore resolved at compile time: the decoder is a straight-line program for
+// that code (the "unrolled decoder" of the fast-SSC literature), with data-dependent branches
+// only where an exactness precondition of a shortcut can fail.
+//
+// Reference semantics (bit-exact): x_run_sn_polar/polar/polar_sc.py -- f = min-sum on clipped
+// inputs (:33-48, min-sum forced at :46), g = (1-2u)x + y unclipped (:49-53), leaf u = 1 iff
+// llr <= 0 (:90-98), partial sums [uL^uR, uR] (:83-89).  FM = 1 selects the exact boxplus f of
+// my_sn/fec/polar/dec.py:39-43 (shortcuts limited to rate-0 and repetition nodes there).
+//
+// Layout ("mirror butterfly").  A wave64 decodes 64/G codewords, G = max(1, n/128) lanes each.
+// Element i of a stage buffer lives in slot i/G of the lane holding residue i mod G.  Residues
+// are placed so that the two residues an f/g pairs at every level of the bottom of the tree
+// (r and r + S/2 inside a size-S block, S <= G) sit in lanes q and q ^ (S-1): the "mirror" of a
+// 2/4/8/16-lane block, which is ONE DPP op (quad_perm / row_half_mirror / row_mirror).  A node
+// of size S <= G is decoded replicated: both lanes of a mirror pair compute the same value
+// (f is symmetric, g adds commutatively, the sign flip is exact), so no gather and no
+// broadcast is ever needed.  Nodes of size >= 2G pair slots j and j + E/2 inside one lane.
+//
+// Exact node shortcuts (what the reference recursion computes, not approximations):
+//   rate-0     beta = 0
+//   REP        u = HD(sum of the node LLRs in SC's pairwise g order), beta = u...u
+//   rate-1     beta = HD(alpha) when no node LLR is exactly 0                  (min-sum only)
+//   SPC        beta = HD(alpha), flip at the unique min |alpha| < llr_max when the parity is
+//              odd; requires no zero LLR and, for odd parity, a unique unclipped min (min-sum only)
+// When a precondition fails anywhere in the wave the node is decoded by the full recursion.
+#pragma once
+#ifndef __HIPCC_RTC__
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#endif
+
+namespace pls {
+
+enum : int { R0 = 0, R1 = 1, REP = 2, SPC = 3, GEN = 4 };
+enum : int { OUT_F32 = 0, OUT_U8 = 1 };
+constexpr int kWaves = 4;  // waves per workgroup
+
+template <bool B, class T, class F>
+struct Cond {
+    using type = T;
+};
+template <class T, class F>
+struct Cond<false, T, F> {
+    using type = F;
+};
+template <int E>
+using Beta = typename Cond<(E <= 32), uint32_t, uint64_t>::type;
+
+template <class C>
+constexpr int nt(int s, int p) {
+    return C::NT[(C::N >> s) + (p >> s)];
+}
+
+template <int E>
+__device__ __forceinline__ Beta<E> ones() {
+    return (Beta<E>)(~(Beta<E>)0 >> (8 * sizeof(Beta<E>) - E));
+}
+
+__device__ __forceinline__ uint32_t fu(float x) { return __float_as_uint(x); }
+__device__ __forceinline__ float uf(uint32_t x) { return __uint_as_float(x); }
+
+// Mirror inside aligned blocks of S lanes: lane q reads lane q ^ (S-1).  One DPP op.
+template <int S>
+__device__ __forceinline__ uint32_t mir(uint32_t v) {
+    static_assert(S == 2 || S == 4 || S == 8 || S == 16, "mirror block");
+    constexpr int ctrl = S == 2 ? 0xB1 : S == 4 ? 0x1B : S == 8 ? 0x141 : 0x140;
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, ctrl, 0xF, 0xF, false);
+}
+template <int S>
+__device__ __forceinline__ float mirf(float v) {
+    return uf(mir<S>(fu(v)));
+}
+
+// f: polar_sc.py:46 (min-sum of clipped inputs) or my_sn dec.py:39-43 (exact boxplus).
+template <int FM>
+__device__ __forceinline__ float fop(float x, float y, float lmax) {
+    if constexpr (FM == 0) {
+        const float m = fminf(fminf(fabsf(x), fabsf(y)), lmax);
+        return uf(fu(m) | ((fu(x) ^ fu(y)) & 0x80000000u));
+    } else {
+        const float xc = fminf(fmaxf(x, -lmax), lmax), yc = fminf(fmaxf(y, -lmax), lmax);
+        float o = logf(1.0f + expf(xc + yc));
+        o -= logf(expf(xc) + expf(yc));
+        return o;
+    }
+}
+// g with the sign flip given as a mask (0 or 0x80000000): (1-2u)x + y, one rounding.
+__device__ __forceinline__ float gop(float x, float y, uint32_t sgn) { return uf(fu(x) ^ sgn) + y; }
+// hard decision of a leaf: u = 1 iff !(llr > 0)  (polar_sc.py:94-97)
+__device__ __forceinline__ uint32_t hd(float x) { return (x > 0.0f) ? 0u : 1u; }
+
+struct Lane {
+    uint32_t lom[5];  // lom[t]: all-ones if this lane holds the low element at level 2^t
+    float lmax;
+};
+
+// ---------------- reductions over the G lanes of a codeword (all lanes get the result) ----
+template <int LG, typename T, typename Op>
+__device__ __forceinline__ T grp(T v, Op op) {
+    if constexpr (LG >= 4) v = op(v, (T)mir<16>((uint32_t)v));
+    if constexpr (LG >= 3) v = op(v, (T)mir<8>((uint32_t)v));
+    if constexpr (LG >= 2) v = op(v, (T)mir<4>((uint32_t)v));
+    if constexpr (LG >= 1) v = op(v, (T)mir<2>((uint32_t)v));
+    return v;
+}
+template <int LG>
+__device__ __forceinline__ float grp_minf(float v) {
+    if constexpr (LG >= 4) v = fminf(v, mirf<16>(v));
+    if constexpr (LG >= 3) v = fminf(v, mirf<8>(v));
+    if constexpr (LG >= 2) v = fminf(v, mirf<4>(v));
+    if constexpr (LG >= 1) v = fminf(v, mirf<2>(v));
+    return v;
+}
+// SC-order sum: level 2^t pairs lanes q and q ^ (2^t - 1) (residues r, r + 2^(t-1)).
+template <int LG>
+__device__ __forceinline__ float grp_sumf(float v) {
+    if constexpr (LG >= 4) v = v + mirf<16>(v);
+    if constexpr (LG >= 3) v = v + mirf<8>(v);
+    if constexpr (LG >= 2) v = v + mirf<4>(v);
+    if constexpr (LG >= 1) v = v + mirf<2>(v);
+    return v;
+}
+
+// ---------------- lane-level nodes: size 2^s <= G, one (replicated) LLR per lane ----------
+template <class C, int s, int P>
+__device__ uint32_t lnode(float a, const Lane& ln);
+
+template <class C, int s, int P>
+__device__ __forceinline__ uint32_t lsplit(float a, const Lane& ln) {
+    constexpr int S = 1 << s;
+    const float y = mirf<S>(a);
+    const uint32_t L = ln.lom[s];
+    uint32_t bl = 0;
+    if constexpr (nt<C>(s - 1, P) != R0) bl = lnode<C, s - 1, P>(fop<C::FM>(a, y, ln.lmax), ln);
+    const uint32_t m = bl << 31;
+    const float x = uf(fu(a) ^ (m & L)) + uf(fu(y) ^ (m & ~L));
+    const uint32_t br = lnode<C, s - 1, P + S / 2>(x, ln);
+    return br ^ (bl & L);
+}
+
+template <class C, int s, int P>
+__device__ __forceinline__ uint32_t lnode(float a, const Lane& ln) {
+    constexpr int T = nt<C>(s, P);
+    if constexpr (T == R0) {
+        return 0u;
+    } else if constexpr (s == 0) {
+        return hd(a);
+    } else if constexpr (T == REP) {
+        float v = a;
+        if constexpr (s >= 4) v = v + mirf<16>(v);
+        if constexpr (s >= 3) v = v + mirf<8>(v);
+        if constexpr (s >= 2) v = v + mirf<4>(v);
+        v = v + mirf<2>(v);
+        return hd(v);
+    } else if constexpr (T == R1 && C::FM == 0) {
+        if (!__any(a == 0.0f)) return fu(a) >> 31;
+        return lsplit<C, s, P>(a, ln);
+    } else if constexpr (T == SPC && C::FM == 0) {
+        const uint32_t b = fu(a) >> 31;
+        const float ab = fabsf(a);
+        uint32_t par = b;
+        float mn = ab;
+        if constexpr (s >= 4) { par ^= mir<16>(par); mn = fminf(mn, mirf<16>(mn)); }
+        if constexpr (s >= 3) { par ^= mir<8>(par); mn = fminf(mn, mirf<8>(mn)); }
+        if constexpr (s >= 2) { par ^= mir<4>(par); mn = fminf(mn, mirf<4>(mn)); }
+        par ^= mir<2>(par);
+        mn = fminf(mn, mirf<2>(mn));
+        const uint32_t eq = (ab == mn) ? 1u : 0u;
+        uint32_t cnt = eq;
+        if constexpr (s >= 4) cnt += mir<16>(cnt);
+        if constexpr (s >= 3) cnt += mir<8>(cnt);
+        if constexpr (s >= 2) cnt += mir<4>(cnt);
+        cnt += mir<2>(cnt);
+        const bool bad = (a == 0.0f) || (par && (cnt != 1u || !(mn < ln.lmax)));
+        if (!__any(bad)) return b ^ (par & eq);
+        return lsplit<C, s, P>(a, ln);
+    } else {
+        return lsplit<C, s, P>(a, ln);
+    }
+}
+
+// ---------------- in-lane nodes: size 2^s >= 2G, E = 2^s / G slots per lane ---------------
+template <class C, int s, int P>
+__device__ Beta<(1 << s) / C::G> node(const float (&a)[(1 << s) / C::G], const Lane& ln);
+
+template <class C, int s, int P>
+__device__ __forceinline__ Beta<(1 << (s - 1)) / C::G> child(const float (&x)[(1 << (s - 1)) / C::G],
+                                                             const Lane& ln) {
+    if constexpr ((1 << (s - 1)) == C::G) {
+        return (Beta<1>)lnode<C, s - 1, P>(x[0], ln);
+    } else {
+        return node<C, s - 1, P>(x, ln);
+    }
+}
+
+template <class C, int s, int P>
+__device__ __forceinline__ Beta<(1 << s) / C::G> split(const float (&a)[(1 << s) / C::G], const Lane& ln) {
+    constexpr int E = (1 << s) / C::G, H = E / 2, h = 1 << (s - 1);
+    using BH = Beta<H>;
+    using BT = Beta<E>;
+    float x[H];
+    BH bl = 0;
+    if constexpr (nt<C>(s - 1, P) != R0) {
+#pragma unroll
+        for (int j = 0; j < H; ++j) x[j] = fop<C::FM>(a[j], a[j + H], ln.lmax);
+        bl = child<C, s, P>(x, ln);
+#pragma unroll
+        for (int j = 0; j < H; ++j) x[j] = gop(a[j], a[j + H], ((uint32_t)(bl >> j) << 31));
+    } else {
+#pragma unroll
+        for (int j = 0; j < H; ++j) x[j] = a[j] + a[j + H];
+    }
+    const BH br = child<C, s, P + h>(x, ln);
+    return (BT)(bl ^ br) | ((BT)br << H);
+}
+
+template <class C, int E>
+__device__ __forceinline__ Beta<E> signs(const float (&a)[E]) {
+    Beta<E> b = 0;
+#pragma unroll
+    for (int j = 0; j < E; ++j) b |= (Beta<E>)(fu(a[j]) >> 31) << j;
+    return b;
+}
+
+template <class C, int s, int P>
+__device__ __forceinline__ Beta<(1 << s) / C::G> node(const float (&a)[(1 << s) / C::G], const Lane& ln) {
+    constexpr int E = (1 << s) / C::G;
+    constexpr int T = nt<C>(s, P);
+    using BT = Beta<E>;
+    if constexpr (T == R0) {
+        return (BT)0;
+    } else if constexpr (T == REP) {
+        float y[E];
+#pragma unroll
+        for (int j = 0; j < E; ++j) y[j] = a[j];
+#pragma unroll
+        for (int hh = E / 2; hh >= 1; hh >>= 1)
+#pragma unroll
+            for (int j = 0; j < hh; ++j) y[j] = y[j] + y[j + hh];
+        const float v = grp_sumf<C::LOG_G>(y[0]);
+        return hd(v) ? ones<E>() : (BT)0;
+    } else if constexpr (T == R1 && C::FM == 0) {
+        bool z = false;
+#pragma unroll
+        for (int j = 0; j < E; ++j) z |= (a[j] == 0.0f);
+        if (!__any(z)) return signs<C, E>(a);
+        return split<C, s, P>(a, ln);
+    } else if constexpr (T == SPC && C::FM == 0) {
+        bool z = false;
+#pragma unroll
+        for (int j = 0; j < E; ++j) z |= (a[j] == 0.0f);
+        BT b = signs<C, E>(a);
+        uint32_t par = (uint32_t)__popcll((unsigned long long)b) & 1u;
+        par = grp<C::LOG_G>(par, [](uint32_t u, uint32_t v) { return u ^ v; });
+        float mn = fabsf(a[0]);
+#pragma unroll
+        for (int j = 1; j < E; ++j) mn = fminf(mn, fabsf(a[j]));
+        mn = grp_minf<C::LOG_G>(mn);
+        BT eqm = 0;
+#pragma unroll
+        for (int j = 0; j < E; ++j) eqm |= (BT)(fabsf(a[j]) == mn) << j;
+        uint32_t cnt = (uint32_t)__popcll((unsigned long long)eqm);
+        cnt = grp<C::LOG_G>(cnt, [](uint32_t u, uint32_t v) { return u + v; });
+        const bool bad = z || (par && (cnt != 1u || !(mn < ln.lmax)));
+        if (!__any(bad)) return par ? (BT)(b ^ eqm) : b;
+        return split<C, s, P>(a, ln);
+    } else {
+        return split<C, s, P>(a, ln);
+    }
+}
+
+// ---------------- root --------------------------------------------------------------------
+// The root's input is the negated channel (polar_sc.py:122), held in VGPRs (NS slots).  The
+// stage LOG_N-1 buffers are "virtual": each of their LLRs is recomputed from two channel values
+// when a pass of the stage-(LOG_N-1) node reads it (f for the left half, g with the left half's
+// partial sums for the right), so the largest stage buffer never occupies registers.
+template <class C>
+__device__ __forceinline__ float valpha(const float (&ch)[C::NS], int side, uint64_t blr, int j, float lmax) {
+    const float x = -ch[j], y = -ch[j + C::NS / 2];
+    return side == 0 ? fop<C::FM>(x, y, lmax) : gop(x, y, (uint32_t)(blr >> j) << 31);
+}
+
+template <class C, int SIDE>
+__device__ __forceinline__ Beta<C::NS / 2> half(const float (&ch)[C::NS], uint64_t blr, const Lane& ln) {
+    constexpr int s = C::LOG_N - 1, P = SIDE << s;
+    constexpr int E = C::NS / 2;  // slots of the stage-(LOG_N-1) node per lane
+    using BT = Beta<E>;
+    constexpr int T = nt<C>(s, P);
+    if constexpr (T == R0) {
+        return (BT)0;
+    } else if constexpr (E == 1) {
+        return (BT)lnode<C, s, P>(valpha<C>(ch, SIDE, blr, 0, ln.lmax), ln);
+    } else if constexpr (T != GEN) {
+        float a[E];
+#pragma unroll
+        for (int j = 0; j < E; ++j) a[j] = valpha<C>(ch, SIDE, blr, j, ln.lmax);
+        return node<C, s, P>(a, ln);
+    } else {
+        constexpr int H = E / 2, h = 1 << (s - 1);
+        using BH = Beta<H>;
+        float x[H];
+        BH bl = 0;
+        if constexpr (nt<C>(s - 1, P) != R0) {
+#pragma unroll
+            for (int j = 0; j < H; ++j)
+                x[j] = fop<C::FM>(valpha<C>(ch, SIDE, blr, j, ln.lmax), valpha<C>(ch, SIDE, blr, j + H, ln.lmax),
+                                  ln.lmax);
+            bl = child<C, s, P>(x, ln);
+        }
+#pragma unroll
+        for (int j = 0; j < H; ++j)
+            x[j] = gop(valpha<C>(ch, SIDE, blr, j, ln.lmax), valpha<C>(ch, SIDE, blr, j + H, ln.lmax),
+                       (uint32_t)(bl >> j) << 31);
+        const BH br = child<C, s, P + h>(x, ln);
+        return (BT)(bl ^ br) | ((BT)br << H);
+    }
+}
+
+// Per-lane constants of the mirror layout.  res(q): residue held by lane q of the group;
+// lom[t]: lane holds the low element of its pair at level 2^t (in its canonical frame).
+template <int LG>
+__device__ __forceinline__ void lane_layout(int q, int& res, uint32_t (&lom)[5]) {
+    int c = q;
+    res = 0;
+#pragma unroll
+    for (int t = 4; t >= 1; --t) lom[t] = 0u;
+#pragma unroll
+    for (int t = LG; t >= 1; --t) {
+        const int S = 1 << t;
+        const bool lo = (c & (S / 2)) == 0;
+        lom[t] = lo ? 0xFFFFFFFFu : 0u;
+        if (!lo) {
+            res += S / 2;
+            c ^= (S - 1);
+        }
+    }
+}
+
+template <class C, int OUT>
+__device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs, void* __restrict__ out,
+                                       const int32_t* __restrict__ info_loc, int k, float lmax,
+                                       uint32_t* __restrict__ ulds) {
+    constexpr int N = C::N, G = C::G, LG = C::LOG_G, NS = C::NS, CW = 64 / G;
+    constexpr int WPL = (NS + 31) / 32;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int q = lane & (G - 1);
+    const int64_t cw0 = ((int64_t)blockIdx.x * kWaves + wave) * CW;
+    const int64_t cw = cw0 + (lane >> LG);
+    const float* ch = llr + (size_t)(cw < bs ? cw : bs - 1) * N;
+
+    Lane ln;
+    int res;
+    lane_layout<LG>(q, res, ln.lom);
+    ln.lom[0] = 0u;
+    ln.lmax = lmax;
+
+    float chv[NS];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) chv[j] = ch[j * G + res];
+
+    uint64_t lo = 0, hi = 0;
+    {
+        using BH = Beta<NS / 2>;
+        const BH bl = half<C, 0>(chv, 0, ln);
+        const BH br = half<C, 1>(chv, (uint64_t)bl, ln);
+        if constexpr (NS / 2 >= 64) {
+            lo = (uint64_t)(bl ^ br);
+            hi = (uint64_t)br;
+        } else {
+            lo = (uint64_t)(bl ^ br) | ((uint64_t)br << (NS / 2));
+        }
+    }
+    // u = x * G_n (G_n is an involution): in-lane spans on the packed slots, then the
+    // cross-lane spans with the mirror DPP (the low element of each pair takes the XOR).
+    {
+        constexpr uint64_t M[6] = {0x5555555555555555ull, 0x3333333333333333ull, 0x0f0f0f0f0f0f0f0full,
+                                   0x00ff00ff00ff00ffull, 0x0000ffff0000ffffull, 0x00000000ffffffffull};
+#pragma unroll
+        for (int t = 0; t < 6; ++t) {
+            if ((1 << t) < NS) {
+                lo ^= (lo >> (1 << t)) & M[t];
+                hi ^= (hi >> (1 << t)) & M[t];
+            }
+        }
+        if constexpr (NS > 64) lo ^= hi;
+        uint32_t w[4] = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+#pragma unroll
+        for (int i = 0; i < WPL; ++i) {
+            if constexpr (LG >= 4) w[i] ^= mir<16>(w[i]) & ln.lom[4];
+            if constexpr (LG >= 3) w[i] ^= mir<8>(w[i]) & ln.lom[3];
+            if constexpr (LG >= 2) w[i] ^= mir<4>(w[i]) & ln.lom[2];
+            if constexpr (LG >= 1) w[i] ^= mir<2>(w[i]) & ln.lom[1];
+        }
+        uint32_t* mine = ulds + (wave * 64 + lane) * WPL;
+#pragma unroll
+        for (int i = 0; i < WPL; ++i) mine[i] = w[i];
+    }
+    __syncthreads();
+    // Information bits (info_pos ascending, polar_sc.py:127) -> coalesced rows.
+    // info_loc[m] = (lane-in-group << 8) | slot of the m-th information position.
+    const uint32_t* ubase = ulds + wave * 64 * WPL;
+    for (int m = lane; m < k; m += 64) {
+        const int loc = info_loc[m];
+        const int l = loc >> 8, slot = loc & 255;
+        const uint32_t* src = ubase + l * WPL + (slot >> 5);
+        const int sh = slot & 31;
+#pragma unroll
+        for (int g = 0; g < CW; ++g) {
+            const int64_t row = cw0 + g;
+            if (row < bs) {
+                const uint32_t bit = (src[g * G * WPL] >> sh) & 1u;
+                if constexpr (OUT == OUT_F32) {
+                    static_cast<float*>(out)[row * k + m] = bit ? 1.0f : 0.0f;
+                } else {
+                    static_cast<uint8_t*>(out)[row * k + m] = (uint8_t)bit;
+                }
+            }
+        }
+    }
+}
+
+}  // namespace pls
+
+// Entry points instantiated per code: the including translation unit defines PlCode first.
+#define PL_SC_STATIC_KERNELS(CODE)                                                                           \
+    extern "C" __global__ __launch_bounds__(64 * pls::kWaves, 2) void pl_sc_static_f32(                      \
+        const float* __restrict__ llr, int64_t bs, void* __restrict__ out, const int32_t* __restrict__ info_loc, \
+        int k, float lmax) {                                                                                 \
+        __shared__ uint32_t ulds[pls::kWaves * 64 * ((CODE::NS + 31) / 32)];                                 \
+        pls::decode<CODE, pls::OUT_F32>(llr, bs, out, info_loc, k, lmax, ulds);                               \
+    }                                                                                                        \
+    extern "C" __global__ __launch_bounds__(64 * pls::kWaves, 2) void pl_sc_static_u8(                       \
+        const float* __restrict__ llr, int64_t bs, void* __restrict__ out, const int32_t* __restrict__ info_loc, \
+        int k, float lmax) {                                                                                 \
+        __shared__ uint32_t ulds[pls::kWaves * 64 * ((CODE::NS + 31) / 32)];                                 \
+        pls::decode<CODE, pls::OUT_U8>(llr, bs, out, info_loc, k, lmax, ulds);                                \
+    }
