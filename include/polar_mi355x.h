@@ -19,6 +19,8 @@
  *                    (+ final sorted msg_pm of _decode_np_batch :178-209)
  *   pl_polar_encode  PolarEncoder.forward x_run_sn_polar/polar/enc.py:30-43
  *                    (butterfly form of my_sn/fec/polar/enc.py:85-96)
+ *   pl_plan_kernel / pl_sc_specialize: no reference counterpart (kernel specialisation per
+ *                    frozen set, the tree walk of polar_sc.py:54-98 resolved at compile time)
  */
 #ifndef POLAR_MI355X_H
 #define POLAR_MI355X_H
@@ -38,6 +40,12 @@ extern "C" {
 #define PL_F_MINSUM 0 /* f = sign*sign*min(|x|,|y|) on clipped inputs (polar_sc.py:46) */
 #define PL_F_EXACT 1  /* f = log(1+e^(x+y)) - log(e^x+e^y) (my_sn dec.py:39-43) */
 
+#define PL_PLAN_GENERIC 1u    /* pl_plan_create flag: never specialise the SC kernel */
+#define PL_PLAN_CACHE_ONLY 2u /* pl_plan_create flag: use a cached specialised kernel, never compile */
+
+#define PL_KERNEL_GENERIC 0     /* pl_plan_kernel kinds */
+#define PL_KERNEL_SPECIALIZED 1
+
 #define PL_OUT_F32 0  /* output 0.0f/1.0f floats, [bs, k] (reference output dtype) */
 #define PL_OUT_U8 1   /* output 0/1 bytes, [bs, k] */
 
@@ -47,7 +55,10 @@ typedef struct pl_plan pl_plan;
  * frozen_mask: HOST pointer to n bytes, nonzero = frozen position (frozen_pos of the reference).
  * list_size:   1 for SC plans; a power of two <= 32 for SCL plans.
  * f_mode:      PL_F_MINSUM or PL_F_EXACT.  llr_max: clipping bound (reference: 30).
- * flags:       reserved, pass 0.
+ * flags:       0, or PL_PLAN_GENERIC / PL_PLAN_CACHE_ONLY.  By default an SC plan (list_size 1)
+ *              runs a kernel specialised to its frozen set: compiled with hiprtc at plan creation
+ *              (seconds) unless a cached code object exists ($PL_KERNEL_CACHE, <library dir>/kcache,
+ *              ~/.cache/polar_mi355x); PL_SC_SPECIALIZE=0 in the environment disables this.
  * n must be a power of two, 2 <= n <= 2048 (SC) / 2 <= n <= 1024 (SCL). */
 int pl_plan_create(pl_plan** out, int32_t n, const uint8_t* frozen_mask, int32_t list_size,
                    int32_t f_mode, float llr_max, uint32_t flags);
@@ -72,6 +83,16 @@ int pl_scl_decode(const pl_plan* plan, const float* llr_logits, int64_t bs, void
 /* Polar encoding with the plan's frozen set: u_bits [bs, k] fp32 0/1 -> codewords [bs, n] fp32. */
 int pl_polar_encode(const pl_plan* plan, const float* u_bits, int64_t bs, float* codewords,
                     void* hip_stream);
+
+/* Which SC kernel a plan launches: *kind = PL_KERNEL_GENERIC / PL_KERNEL_SPECIALIZED; path
+ * (nullable) receives the code object file of a specialised kernel. */
+int pl_plan_kernel(const pl_plan* plan, int32_t* kind, char* path, size_t path_len);
+
+/* Compile (or find) the specialised SC kernel of a code into cache_dir (NULL = default cache)
+ * without touching a GPU; path (nullable) receives the code object file.  Used to pre-build the
+ * kernels of known codes. */
+int pl_sc_specialize(int32_t n, const uint8_t* frozen_mask, int32_t f_mode, const char* cache_dir,
+                     char* path, size_t path_len);
 
 const char* pl_last_error_string(void);
 const char* pl_version(void);

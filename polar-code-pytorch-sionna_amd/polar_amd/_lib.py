@@ -17,6 +17,8 @@ LIB_PATH = os.path.join(_HERE, "libpolar_mi355x.so")
 PL_OK, PL_EINVAL, PL_EHIP, PL_ENOTSUP = 0, -1, -2, -3
 PL_F_MINSUM, PL_F_EXACT = 0, 1
 PL_OUT_F32, PL_OUT_U8 = 0, 1
+PL_PLAN_GENERIC, PL_PLAN_CACHE_ONLY = 1, 2
+PL_KERNEL_GENERIC, PL_KERNEL_SPECIALIZED = 0, 1
 
 _lock = threading.Lock()
 _lib = None
@@ -36,10 +38,12 @@ def _declare(L):
     L.pl_scl_workspace_size.restype = ctypes.c_size_t
     L.pl_scl_decode.argtypes = [P, P, i64, P, i32, P, P, ctypes.c_size_t, P]
     L.pl_polar_encode.argtypes = [P, P, i64, P, P]
+    L.pl_plan_kernel.argtypes = [P, P, ctypes.c_char_p, ctypes.c_size_t]
+    L.pl_sc_specialize.argtypes = [i32, P, i32, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
     L.pl_last_error_string.restype = ctypes.c_char_p
     L.pl_version.restype = ctypes.c_char_p
     for f in (L.pl_plan_create, L.pl_plan_destroy, L.pl_plan_info, L.pl_sc_decode, L.pl_scl_decode,
-              L.pl_polar_encode):
+              L.pl_polar_encode, L.pl_plan_kernel, L.pl_sc_specialize):
         f.restype = ctypes.c_int
     return L
 
@@ -60,7 +64,7 @@ def lib():
 
 EXPORTED_SYMBOLS = ("pl_plan_create", "pl_plan_destroy", "pl_plan_info", "pl_sc_decode",
                     "pl_scl_workspace_size", "pl_scl_decode", "pl_polar_encode",
-                    "pl_last_error_string", "pl_version")
+                    "pl_plan_kernel", "pl_sc_specialize", "pl_last_error_string", "pl_version")
 
 
 def check(rc, what):
@@ -78,13 +82,15 @@ def current_stream_ptr(device):
 class Plan:
     """Owning wrapper of a pl_plan* (immutable, usable from any stream)."""
 
-    def __init__(self, n, frozen_mask_u8, list_size=1, f_mode=PL_F_MINSUM, llr_max=30.0):
+    def __init__(self, n, frozen_mask_u8, list_size=1, f_mode=PL_F_MINSUM, llr_max=30.0, flags=0):
+        """flags: 0 (SC plans get a kernel specialised to the frozen set), PL_PLAN_GENERIC or
+        PL_PLAN_CACHE_ONLY (see include/polar_mi355x.h)."""
         import numpy as np
         mask = np.ascontiguousarray(frozen_mask_u8, dtype=np.uint8)
         assert mask.shape == (n,)
         self._h = ctypes.c_void_p()
         check(lib().pl_plan_create(ctypes.byref(self._h), int(n), mask.ctypes.data_as(ctypes.c_void_p),
-                                   int(list_size), int(f_mode), float(llr_max), 0), "pl_plan_create")
+                                   int(list_size), int(f_mode), float(llr_max), int(flags)), "pl_plan_create")
         n_, k_, l_ = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         check(lib().pl_plan_info(self._h, ctypes.byref(n_), ctypes.byref(k_), ctypes.byref(l_)), "pl_plan_info")
         self.n, self.k, self.list_size = n_.value, k_.value, l_.value
@@ -92,6 +98,12 @@ class Plan:
     @property
     def handle(self):
         return self._h
+
+    def kernel(self):
+        """('specialized' | 'generic', code-object path or '') of the SC kernel this plan runs."""
+        kind, buf = ctypes.c_int32(), ctypes.create_string_buffer(4096)
+        check(lib().pl_plan_kernel(self._h, ctypes.byref(kind), buf, 4096), "pl_plan_kernel")
+        return ("specialized" if kind.value == PL_KERNEL_SPECIALIZED else "generic"), buf.value.decode()
 
     def __del__(self):
         h = getattr(self, "_h", None)

@@ -1,26 +1,29 @@
-"""Build libpolar_mi355x.so (the HIP kernels + C ABI) in-tree for gfx950.
+"""Build libpolar_mi355x.so (the HIP kernels + C ABI) in-tree for gfx950, and pre-build the
+code-specialised SC kernels of the reference's codes into polar_amd/kcache/.
 
     python -m polar_amd.build            # from polar-code-pytorch-sionna_amd/
 
-hipcc cross-compiles for gfx950 without a GPU, so this runs in the build container; the
-resulting .so travels to the GPU box with the repository snapshot.
+hipcc (and hiprtc) cross-compile for gfx950 without a GPU, so this runs in the build container;
+the library and the kernel cache travel to the GPU box with the repository snapshot.
 """
 import os
 import shutil
 import subprocess
 import sys
-from concurrent.futures import ThreadPoolExecutor
+from concurrent.futures import ProcessPoolExecutor, ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "_obj")
 LIB = os.path.join(HERE, "libpolar_mi355x.so")
-SOURCES = ["sc_kernel.hip", "scl_kernel.hip", "encode_kernel.hip", "capi.cpp"]
+KCACHE = os.path.join(HERE, "kcache")
+SOURCES = ["sc_kernel.hip", "scl_kernel.hip", "encode_kernel.hip", "capi.cpp", "jit.cpp"]
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
 
 def _hipcc():
-    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+    for cand in (os.environ.get("HIPCC"), os.path.join(ROCM, "bin", "hipcc"), shutil.which("hipcc")):
         if cand and os.path.exists(cand):
             return cand
     raise RuntimeError("hipcc not found; the MI355X decoder library cannot be built")
@@ -33,20 +36,35 @@ def _needs(obj, src, deps):
     return any(os.path.getmtime(d) > t for d in [src] + deps)
 
 
+def _embed_static_source():
+    """sc_static.h as a C++ raw string literal (the hiprtc source of the specialised kernels)."""
+    src = open(os.path.join(CSRC, "sc_static.h")).read()
+    assert ")PLSRC\"" not in src
+    inc = os.path.join(OBJ, "sc_static_src.inc")
+    text = 'R"PLSRC(' + src + ')PLSRC"\n'
+    if not os.path.exists(inc) or open(inc).read() != text:
+        with open(inc, "w") as f:
+            f.write(text)
+    return inc
+
+
 def build(force=False, verbose=False):
     hipcc = _hipcc()
     os.makedirs(OBJ, exist_ok=True)
+    inc = _embed_static_source()
     deps = [os.path.join(CSRC, "plan.h"),
             os.path.join(HERE, "..", "..", "include", "polar_mi355x.h")]
     jobs = []
     for s in SOURCES:
         src = os.path.join(CSRC, s)
         obj = os.path.join(OBJ, s + ".o")
-        if force or _needs(obj, src, deps):
+        extra = [inc] if s == "jit.cpp" else []
+        if force or _needs(obj, src, deps + extra):
             lang = ["-x", "hip"] if s.endswith(".cpp") else []
             cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-                   "-ffp-contract=off", *lang, "-c", src, "-o", obj]
+                   "-ffp-contract=off", f"-I{OBJ}", *lang, "-c", src, "-o", obj]
             jobs.append(cmd)
+
     def run(cmd):
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
@@ -57,12 +75,65 @@ def build(force=False, verbose=False):
         list(ex.map(run, jobs))
     objs = [os.path.join(OBJ, s + ".o") for s in SOURCES]
     if force or jobs or not os.path.exists(LIB):
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", LIB]
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, f"-L{ROCM}/lib",
+               f"-Wl,-rpath,{ROCM}/lib", "-lhiprtc", "-o", LIB]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed:\n" + r.stdout + r.stderr)
     return LIB
 
 
+def _specialize_one(args):
+    """Worker: compile one code's specialised SC kernel into KCACHE (fresh process, no GPU)."""
+    import ctypes
+    import numpy as np
+    n, mask_bytes, f_mode = args
+    L = ctypes.CDLL(LIB)
+    L.pl_sc_specialize.argtypes = [ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32, ctypes.c_char_p,
+                                   ctypes.c_char_p, ctypes.c_size_t]
+    L.pl_last_error_string.restype = ctypes.c_char_p
+    buf = ctypes.create_string_buffer(4096)
+    rc = L.pl_sc_specialize(n, mask_bytes, f_mode, KCACHE.encode(), buf, 4096)
+    if rc != 0:
+        return f"n={n} f_mode={f_mode}: {L.pl_last_error_string().decode(errors='replace')[:500]}"
+    return None
+
+
+def prebuild_codes(codes, workers=None):
+    """Compile the specialised SC kernels of `codes` = [(frozen_mask uint8[n], f_mode)] into
+    KCACHE (content-addressed: unchanged codes are found and skipped)."""
+    os.makedirs(KCACHE, exist_ok=True)
+    jobs = [(len(m), bytes(bytearray(m)), int(fm)) for m, fm in codes]
+    jobs.sort(key=lambda j: -j[0])  # longest compiles first
+    workers = workers or min(8, os.cpu_count() or 1)
+    with ProcessPoolExecutor(max_workers=workers) as ex:
+        errs = [e for e in ex.map(_specialize_one, jobs) if e]
+    if errs:
+        raise RuntimeError("specialised SC kernel pre-build failed:\n" + "\n".join(errs))
+
+
+def reference_codes():
+    """The codes the reference harness and this package's tests/bench use: every pinned
+    reference frozen set with n <= 2048 (min-sum), and the golden shapes in exact-f mode."""
+    import numpy as np
+    data = os.path.join(HERE, "data", "frozen_sets.npz")
+    out = []
+    with np.load(data) as d:
+        for key in d.files:
+            k, n = (int(v[1:]) for v in key.split("_"))
+            if n > 2048:
+                continue
+            m = np.zeros(n, dtype=np.uint8)
+            m[d[key].astype(np.int64)] = 1
+            out.append((m, 0))
+            if (k, n) in ((2, 4), (4, 8), (8, 16), (16, 32), (16, 64), (32, 64), (48, 64), (128, 256),
+                          (256, 512), (512, 1024), (1024, 2048)):
+                out.append((m, 1))
+    return out
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+    if "--no-kernels" not in sys.argv:
+        prebuild_codes(reference_codes())
+        print("kcache:", len(os.listdir(KCACHE)), "code objects")

@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -46,6 +48,8 @@ int upload(T** dst, const std::vector<T>& src) {
 
 void free_plan(pl_plan* p) {
     if (!p) return;
+    pl::detach_static(p);
+    (void)hipFree(p->d_info_loc);
     (void)hipFree(p->d_frozen_words);
     (void)hipFree(p->d_rate0_words);
     (void)hipFree(p->d_type_words);
@@ -140,6 +144,21 @@ int pl_plan_create(pl_plan** out, int32_t n, const uint8_t* frozen_mask, int32_t
         free_plan(p);
         return r;
     }
+    // SC plans get a kernel specialised to this frozen set (jit.cpp), unless the caller or
+    // PL_SC_SPECIALIZE=0 asks for the generic one.  Failure to specialise is not an error: the
+    // generic kernel is exact too; pl_plan_kernel() reports which one the plan uses.
+    const char* env = getenv("PL_SC_SPECIALIZE");
+    const bool want = list_size == 1 && !(flags & PL_PLAN_GENERIC) && !(env && env[0] == '0');
+    if (want) {
+        const std::string saved = g_last_error;
+        const int rs = pl::attach_static(p, frozen_mask, !(flags & PL_PLAN_CACHE_ONLY));
+        if (rs != PL_OK) {
+            if (getenv("PL_VERBOSE")) fprintf(stderr, "polar_mi355x: generic SC kernel (%s)\n", g_last_error.c_str());
+            pl::detach_static(p);
+            (void)hipGetLastError();
+        }
+        g_last_error = saved;
+    }
     *out = p;
     return PL_OK;
 }
@@ -169,6 +188,7 @@ int pl_sc_decode(const pl_plan* p, const float* llr, int64_t bs, void* out, int3
         pl::set_error("pl_sc_decode: unknown out_kind");
         return PL_EINVAL;
     }
+    if (p->sc_module) return pl::launch_sc_static(p, llr, bs, out, out_kind, static_cast<hipStream_t>(stream));
     return pl::launch_sc(p, llr, bs, out, out_kind, static_cast<hipStream_t>(stream));
 }
 

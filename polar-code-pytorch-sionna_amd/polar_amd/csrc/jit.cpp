@@ -1,0 +1,302 @@
+// jit.cpp -- code-specialised SC kernels: source generation, hiprtc compilation, a
+// content-addressed code-object cache, module loading and launch.
+//
+// A plan for an SC code (list_size 1) gets its own kernel: sc_static.h instantiated with the
+// code's node-type table (R0/R1/REP/SPC/GEN for every node of the decoding tree), so every
+// node-type decision of the reference recursion (x_run_sn_polar/polar/polar_sc.py:54-98) is
+// resolved at compile time.  Code objects are cached by a hash of the generated source and
+// the compile options; build.py pre-compiles the codes the reference harness uses, so plans
+// for them load without compiling.  If hiprtc is unavailable or fails, the plan keeps the
+// generic kernel (sc_kernel.hip), which is equally exact.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+#include <stdint.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../../include/polar_mi355x.h"
+#include "plan.h"
+
+namespace {
+
+const char kStaticSrc[] =
+#include "sc_static_src.inc"
+    ;
+
+const char* kOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off"};
+constexpr int kNumOpts = sizeof(kOpts) / sizeof(kOpts[0]);
+
+enum : int { R0 = 0, R1 = 1, REP = 2, SPC = 3, GEN = 4 };
+
+uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
+    for (unsigned char c : s) {
+        h ^= c;
+        h *= 1099511628211ull;
+    }
+    return h;
+}
+
+int log2_exact(int n) {
+    int s = 0;
+    while ((1 << s) < n) ++s;
+    return (1 << s) == n ? s : -1;
+}
+
+std::string lib_dir() {
+    Dl_info info;
+    if (dladdr(reinterpret_cast<const void*>(&fnv1a), &info) && info.dli_fname) {
+        std::string p(info.dli_fname);
+        const size_t cut = p.find_last_of('/');
+        if (cut != std::string::npos) return p.substr(0, cut);
+    }
+    return ".";
+}
+
+bool mkdirs(const std::string& d) {
+    if (d.empty()) return false;
+    struct stat st;
+    if (stat(d.c_str(), &st) == 0) return S_ISDIR(st.st_mode);
+    const size_t cut = d.find_last_of('/');
+    if (cut != std::string::npos && cut > 0) mkdirs(d.substr(0, cut));
+    return mkdir(d.c_str(), 0755) == 0 || errno == EEXIST;
+}
+
+// Cache directories, in lookup order: $PL_KERNEL_CACHE, <dir of this library>/kcache (pre-built
+// by build.py, travels with the package), $HOME/.cache/polar_mi355x.
+std::vector<std::string> cache_dirs() {
+    std::vector<std::string> d;
+    if (const char* e = getenv("PL_KERNEL_CACHE")) {
+        if (*e) d.push_back(e);
+    }
+    d.push_back(lib_dir() + "/kcache");
+    if (const char* h = getenv("HOME")) d.push_back(std::string(h) + "/.cache/polar_mi355x");
+    return d;
+}
+
+bool read_file(const std::string& path, std::vector<char>& out) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return false;
+    out.assign(std::istreambuf_iterator<char>(f), std::istreambuf_iterator<char>());
+    return !out.empty();
+}
+
+bool write_file_atomic(const std::string& dir, const std::string& name, const std::vector<char>& data) {
+    if (!mkdirs(dir) || access(dir.c_str(), W_OK) != 0) return false;
+    const std::string tmp = dir + "/." + name + "." + std::to_string(getpid()) + ".tmp";
+    {
+        std::ofstream f(tmp, std::ios::binary);
+        if (!f) return false;
+        f.write(data.data(), (std::streamsize)data.size());
+        if (!f) return false;
+    }
+    return rename(tmp.c_str(), (dir + "/" + name).c_str()) == 0;
+}
+
+}  // namespace
+
+namespace pl {
+
+// Node types in heap order: node of size 2^s at position p -> index (n >> s) + (p >> s).
+std::vector<uint8_t> node_types(int n, const uint8_t* frozen) {
+    const int log_n = log2_exact(n);
+    std::vector<uint8_t> nt(2 * (size_t)n, R0);
+    for (int s = 0; s <= log_n; ++s) {
+        const int S = 1 << s;
+        for (int p = 0; p < n; p += S) {
+            int nfz = 0;
+            for (int i = p; i < p + S; ++i) nfz += frozen[i] != 0;
+            int t;
+            if (nfz == S) t = R0;
+            else if (nfz == 0) t = R1;
+            else if (S >= 2 && nfz == S - 1 && !frozen[p + S - 1]) t = REP;
+            else if (S >= 2 && nfz == 1 && frozen[p]) t = SPC;
+            else t = GEN;
+            nt[(size_t)(n >> s) + (size_t)(p >> s)] = (uint8_t)t;
+        }
+    }
+    return nt;
+}
+
+int static_log_g(int log_n) { return log_n > 7 ? log_n - 7 : 0; }
+
+// Lane of the codeword group holding residue r (mirror-butterfly layout of sc_static.h).
+int mirror_lane(int G, int r) {
+    if (G == 1) return 0;
+    return r < G / 2 ? mirror_lane(G / 2, r) : G - 1 - mirror_lane(G / 2, r - G / 2);
+}
+
+std::string static_source(int n, const uint8_t* frozen, int f_mode) {
+    const int log_n = log2_exact(n), lg = static_log_g(log_n);
+    const std::vector<uint8_t> nt = node_types(n, frozen);
+    std::ostringstream o;
+    o << kStaticSrc << "\nstruct PlCode {\n  static constexpr int N = " << n << ", LOG_N = " << log_n
+      << ", LOG_G = " << lg << ", G = " << (1 << lg) << ", NS = " << (n >> lg) << ", FM = " << f_mode
+      << ";\n  static constexpr unsigned char NT[" << nt.size() << "] = {";
+    for (size_t i = 0; i < nt.size(); ++i) o << (i ? "," : "") << (int)nt[i];
+    o << "};\n};\nPL_SC_STATIC_KERNELS(PlCode)\n";
+    return o.str();
+}
+
+std::string cache_name(const std::string& src) {
+    std::string key = src;
+    for (int i = 0; i < kNumOpts; ++i) key += std::string("\n//opt ") + kOpts[i];
+    int major = 0, minor = 0;
+    if (hiprtcVersion(&major, &minor) == HIPRTC_SUCCESS) key += "\n//hiprtc " + std::to_string(major) + "." + std::to_string(minor);
+    char buf[32];
+    snprintf(buf, sizeof buf, "sc_%016llx.co", (unsigned long long)fnv1a(key));
+    return buf;
+}
+
+// Compile (or find in a cache) the code object of one code.  No GPU needed.
+int specialize(int n, const uint8_t* frozen, int f_mode, const char* forced_dir, bool allow_compile,
+               std::vector<char>& image, std::string& path) {
+    const std::string src = static_source(n, frozen, f_mode);
+    const std::string name = cache_name(src);
+    std::vector<std::string> dirs;
+    if (forced_dir && *forced_dir) dirs.push_back(forced_dir);
+    else dirs = cache_dirs();
+    for (const auto& d : dirs) {
+        if (read_file(d + "/" + name, image)) {
+            path = d + "/" + name;
+            return PL_OK;
+        }
+    }
+    if (!allow_compile) {
+        set_error("specialised SC kernel not in cache: " + name);
+        return PL_ENOTSUP;
+    }
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "pl_sc_static.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+        set_error("hiprtcCreateProgram failed");
+        return PL_ENOTSUP;
+    }
+    const hiprtcResult rc = hiprtcCompileProgram(prog, kNumOpts, kOpts);
+    if (rc != HIPRTC_SUCCESS) {
+        size_t ls = 0;
+        hiprtcGetProgramLogSize(prog, &ls);
+        std::string log(ls, '\0');
+        if (ls) hiprtcGetProgramLog(prog, &log[0]);
+        hiprtcDestroyProgram(&prog);
+        set_error("hiprtc compile of the specialised SC kernel failed: " + log.substr(0, 2000));
+        return PL_ENOTSUP;
+    }
+    size_t cs = 0;
+    hiprtcGetCodeSize(prog, &cs);
+    image.assign(cs, 0);
+    hiprtcGetCode(prog, image.data());
+    hiprtcDestroyProgram(&prog);
+    path.clear();
+    for (const auto& d : dirs) {
+        if (write_file_atomic(d, name, image)) {
+            path = d + "/" + name;
+            break;
+        }
+    }
+    return PL_OK;
+}
+
+// Per-plan setup: info_loc table + module (called from pl_plan_create for SC plans).
+int attach_static(pl_plan* p, const uint8_t* frozen, bool allow_compile) {
+    std::vector<char> image;
+    std::string path;
+    int r = specialize(p->n, frozen, p->f_mode, nullptr, allow_compile, image, path);
+    if (r) return r;
+    hipModule_t mod;
+    r = check_hip(hipModuleLoadData(&mod, image.data()), "hipModuleLoadData(specialised SC kernel)");
+    if (r) return r;
+    hipFunction_t f32, u8;
+    r = check_hip(hipModuleGetFunction(&f32, mod, "pl_sc_static_f32"), "hipModuleGetFunction");
+    if (!r) r = check_hip(hipModuleGetFunction(&u8, mod, "pl_sc_static_u8"), "hipModuleGetFunction");
+    const int G = 1 << static_log_g(p->log_n);
+    std::vector<int32_t> loc;
+    for (int i = 0; i < p->n; ++i)
+        if (!frozen[i]) loc.push_back((mirror_lane(G, i % G) << 8) | (i / G));
+    while (loc.size() % 4) loc.push_back(0);  // int4 reads of the table
+    if (!r && !loc.empty()) {
+        r = check_hip(hipMalloc(reinterpret_cast<void**>(&p->d_info_loc), loc.size() * sizeof(int32_t)),
+                      "hipMalloc(info_loc)");
+        if (!r)
+            r = check_hip(hipMemcpy(p->d_info_loc, loc.data(), loc.size() * sizeof(int32_t), hipMemcpyHostToDevice),
+                          "hipMemcpy(info_loc)");
+    }
+    if (r) {
+        (void)hipModuleUnload(mod);
+        return r;
+    }
+    p->sc_module = mod;
+    p->sc_fn_f32 = f32;
+    p->sc_fn_u8 = u8;
+    p->kernel_path = path;
+    return PL_OK;
+}
+
+void detach_static(pl_plan* p) {
+    if (p->sc_module) (void)hipModuleUnload(p->sc_module);
+    p->sc_module = nullptr;
+    p->sc_fn_f32 = p->sc_fn_u8 = nullptr;
+}
+
+int launch_sc_static(const pl_plan* p, const float* llr, int64_t bs, void* out, int out_kind, hipStream_t st) {
+    if (bs == 0 || p->k == 0) return PL_OK;
+    const int G = 1 << static_log_g(p->log_n);
+    const int64_t per_block = 4 * (64 / G);  // pls::kWaves codeword groups of 64/G
+    const int64_t blocks = (bs + per_block - 1) / per_block;
+    if (blocks > 0x7fffffffLL) {
+        set_error("SC decode: batch too large for one launch");
+        return PL_EINVAL;
+    }
+    const float lmax = p->llr_max;
+    int k = p->k;
+    const int32_t* loc = p->d_info_loc;
+    void* args[] = {(void*)&llr, (void*)&bs, (void*)&out, (void*)&loc, (void*)&k, (void*)&lmax};
+    hipFunction_t fn = out_kind == PL_OUT_F32 ? p->sc_fn_f32 : p->sc_fn_u8;
+    return check_hip(hipModuleLaunchKernel(fn, (unsigned)blocks, 1, 1, 256, 1, 1, 0, st, args, nullptr),
+                     "SC decode launch (specialised)");
+}
+
+}  // namespace pl
+
+extern "C" {
+
+int pl_sc_specialize(int32_t n, const uint8_t* frozen_mask, int32_t f_mode, const char* cache_dir, char* path_out,
+                     size_t path_len) {
+    if (!frozen_mask || log2_exact(n) < 1 || log2_exact(n) > 11 || (f_mode != PL_F_MINSUM && f_mode != PL_F_EXACT)) {
+        pl::set_error("pl_sc_specialize: bad arguments");
+        return PL_EINVAL;
+    }
+    std::vector<char> image;
+    std::string path;
+    const int r = pl::specialize(n, frozen_mask, f_mode, cache_dir, true, image, path);
+    if (r) return r;
+    if (path_out && path_len) {
+        strncpy(path_out, path.c_str(), path_len - 1);
+        path_out[path_len - 1] = 0;
+    }
+    return PL_OK;
+}
+
+int pl_plan_kernel(const pl_plan* p, int32_t* kind, char* path_out, size_t path_len) {
+    if (!p) {
+        pl::set_error("pl_plan_kernel: null plan");
+        return PL_EINVAL;
+    }
+    if (kind) *kind = p->sc_module ? PL_KERNEL_SPECIALIZED : PL_KERNEL_GENERIC;
+    if (path_out && path_len) {
+        strncpy(path_out, p->kernel_path.c_str(), path_len - 1);
+        path_out[path_len - 1] = 0;
+    }
+    return PL_OK;
+}
+
+}  // extern "C"

@@ -16,6 +16,11 @@ struct pl_plan {
     int32_t type_stride = 64;            //   node flags, same bit indexing as d_rate0_words
     int32_t* d_info_pos = nullptr;       // k ascending information positions
     int32_t* d_info_rank = nullptr;      // n entries: rank among info positions, -1 if frozen
+    // Code-specialised SC kernel (jit.cpp / sc_static.h); null module = generic kernel.
+    int32_t* d_info_loc = nullptr;       // k (padded to 4): (lane-in-group << 8) | slot of info bit m
+    hipModule_t sc_module = nullptr;
+    hipFunction_t sc_fn_f32 = nullptr, sc_fn_u8 = nullptr;
+    std::string kernel_path;             // code object the module came from
 };
 
 namespace pl {
@@ -29,4 +34,10 @@ size_t scl_workspace_size(const pl_plan* plan, int64_t bs);
 int launch_scl(const pl_plan* plan, const float* llr, int64_t bs, void* out, int out_kind,
                double* out_pm, void* ws, size_t ws_bytes, hipStream_t stream);
 int launch_encode(const pl_plan* plan, const float* u, int64_t bs, float* cw, hipStream_t stream);
+
+// Code-specialised SC kernels (jit.cpp)
+int attach_static(pl_plan* plan, const uint8_t* frozen_mask, bool allow_compile);
+void detach_static(pl_plan* plan);
+int launch_sc_static(const pl_plan* plan, const float* llr, int64_t bs, void* out, int out_kind,
+                     hipStream_t stream);
 }  // namespace pl

@@ -31,10 +31,18 @@
 //   SPC        beta = HD(alpha), flip at the unique min |alpha| < llr_max when the parity is
 //              odd; requires no zero LLR and, for odd parity, a unique unclipped min (min-sum only)
 // When a precondition fails anywhere in the wave the node is decoded by the full recursion.
-#pragma once
+#ifndef PL_SC_STATIC_H
+#define PL_SC_STATIC_H
 #ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#else  // hiprtc: no libc headers
+typedef unsigned char uint8_t;
+typedef int int32_t;
+typedef unsigned int uint32_t;
+typedef long long int64_t;
+typedef unsigned long long uint64_t;
+typedef unsigned long uintptr_t;
 #endif
 
 namespace pls {
@@ -72,7 +80,8 @@ template <int S>
 __device__ __forceinline__ uint32_t mir(uint32_t v) {
     static_assert(S == 2 || S == 4 || S == 8 || S == 16, "mirror block");
     constexpr int ctrl = S == 2 ? 0xB1 : S == 4 ? 0x1B : S == 8 ? 0x141 : 0x140;
-    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, ctrl, 0xF, 0xF, false);
+    // mov_dpp (no "old" operand, bound_ctrl) lets the DPP combiner fold the move into its user.
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, ctrl, 0xF, 0xF, true);
 }
 template <int S>
 __device__ __forceinline__ float mirf(float v) {
@@ -109,14 +118,6 @@ __device__ __forceinline__ T grp(T v, Op op) {
     if constexpr (LG >= 3) v = op(v, (T)mir<8>((uint32_t)v));
     if constexpr (LG >= 2) v = op(v, (T)mir<4>((uint32_t)v));
     if constexpr (LG >= 1) v = op(v, (T)mir<2>((uint32_t)v));
-    return v;
-}
-template <int LG>
-__device__ __forceinline__ float grp_minf(float v) {
-    if constexpr (LG >= 4) v = fminf(v, mirf<16>(v));
-    if constexpr (LG >= 3) v = fminf(v, mirf<8>(v));
-    if constexpr (LG >= 2) v = fminf(v, mirf<4>(v));
-    if constexpr (LG >= 1) v = fminf(v, mirf<2>(v));
     return v;
 }
 // SC-order sum: level 2^t pairs lanes q and q ^ (2^t - 1) (residues r, r + 2^(t-1)).
@@ -164,22 +165,22 @@ __device__ __forceinline__ uint32_t lnode(float a, const Lane& ln) {
         if (!__any(a == 0.0f)) return fu(a) >> 31;
         return lsplit<C, s, P>(a, ln);
     } else if constexpr (T == SPC && C::FM == 0) {
+        // magnitudes compared as integers (non-negative floats order like their bit patterns)
         const uint32_t b = fu(a) >> 31;
-        const float ab = fabsf(a);
-        uint32_t par = b;
-        float mn = ab;
-        if constexpr (s >= 4) { par ^= mir<16>(par); mn = fminf(mn, mirf<16>(mn)); }
-        if constexpr (s >= 3) { par ^= mir<8>(par); mn = fminf(mn, mirf<8>(mn)); }
-        if constexpr (s >= 2) { par ^= mir<4>(par); mn = fminf(mn, mirf<4>(mn)); }
+        const uint32_t ab = fu(a) & 0x7FFFFFFFu;
+        uint32_t par = b, mn = ab;
+        if constexpr (s >= 4) { par ^= mir<16>(par); mn = min(mn, mir<16>(mn)); }
+        if constexpr (s >= 3) { par ^= mir<8>(par); mn = min(mn, mir<8>(mn)); }
+        if constexpr (s >= 2) { par ^= mir<4>(par); mn = min(mn, mir<4>(mn)); }
         par ^= mir<2>(par);
-        mn = fminf(mn, mirf<2>(mn));
+        mn = min(mn, mir<2>(mn));
         const uint32_t eq = (ab == mn) ? 1u : 0u;
         uint32_t cnt = eq;
         if constexpr (s >= 4) cnt += mir<16>(cnt);
         if constexpr (s >= 3) cnt += mir<8>(cnt);
         if constexpr (s >= 2) cnt += mir<4>(cnt);
         cnt += mir<2>(cnt);
-        const bool bad = (a == 0.0f) || (par && (cnt != 1u || !(mn < ln.lmax)));
+        const bool bad = (ab == 0u) | ((par != 0u) & ((cnt != 1u) | (mn >= fu(ln.lmax))));
         if (!__any(bad)) return b ^ (par & eq);
         return lsplit<C, s, P>(a, ln);
     } else {
@@ -256,20 +257,20 @@ __device__ __forceinline__ Beta<(1 << s) / C::G> node(const float (&a)[(1 << s) 
     } else if constexpr (T == SPC && C::FM == 0) {
         bool z = false;
 #pragma unroll
-        for (int j = 0; j < E; ++j) z |= (a[j] == 0.0f);
+        for (int j = 0; j < E; ++j) z |= ((fu(a[j]) & 0x7FFFFFFFu) == 0u);
         BT b = signs<C, E>(a);
         uint32_t par = (uint32_t)__popcll((unsigned long long)b) & 1u;
         par = grp<C::LOG_G>(par, [](uint32_t u, uint32_t v) { return u ^ v; });
-        float mn = fabsf(a[0]);
+        uint32_t mn = fu(a[0]) & 0x7FFFFFFFu;
 #pragma unroll
-        for (int j = 1; j < E; ++j) mn = fminf(mn, fabsf(a[j]));
-        mn = grp_minf<C::LOG_G>(mn);
+        for (int j = 1; j < E; ++j) mn = min(mn, fu(a[j]) & 0x7FFFFFFFu);
+        mn = grp<C::LOG_G>(mn, [](uint32_t u, uint32_t v) { return min(u, v); });
         BT eqm = 0;
 #pragma unroll
-        for (int j = 0; j < E; ++j) eqm |= (BT)(fabsf(a[j]) == mn) << j;
+        for (int j = 0; j < E; ++j) eqm |= (BT)((fu(a[j]) & 0x7FFFFFFFu) == mn) << j;
         uint32_t cnt = (uint32_t)__popcll((unsigned long long)eqm);
         cnt = grp<C::LOG_G>(cnt, [](uint32_t u, uint32_t v) { return u + v; });
-        const bool bad = z || (par && (cnt != 1u || !(mn < ln.lmax)));
+        const bool bad = z | ((par != 0u) & ((cnt != 1u) | (mn >= fu(ln.lmax))));
         if (!__any(bad)) return par ? (BT)(b ^ eqm) : b;
         return split<C, s, P>(a, ln);
     } else {
@@ -344,6 +345,16 @@ __device__ __forceinline__ void lane_layout(int q, int& res, uint32_t (&lom)[5])
     }
 }
 
+#ifndef PL_SC_ROOT_MODE
+#define PL_SC_ROOT_MODE 0
+#endif
+#ifndef PL_SC_MINW
+#define PL_SC_MINW 2
+#endif
+#ifndef PL_SC_STAMPS
+#define PL_SC_STAMPS 0
+#endif
+
 template <class C, int OUT>
 __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs, void* __restrict__ out,
                                        const int32_t* __restrict__ info_loc, int k, float lmax,
@@ -362,11 +373,20 @@ __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs
     ln.lom[0] = 0u;
     ln.lmax = lmax;
 
+#if PL_SC_STAMPS
+    // diagnostic build: per-wave clock stamps into the output's tail (tools/static_probe.py)
+    uint64_t st0 = __builtin_amdgcn_s_memtime();
+#endif
+    uint64_t lo = 0, hi = 0;
+#if PL_SC_ROOT_MODE == 0
     float chv[NS];
 #pragma unroll
     for (int j = 0; j < NS; ++j) chv[j] = ch[j * G + res];
-
-    uint64_t lo = 0, hi = 0;
+#if PL_SC_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+    for (int j = 0; j < NS; ++j) asm volatile("" : "+v"(chv[j]));
+    uint64_t st1 = __builtin_amdgcn_s_memtime();
+#endif
     {
         using BH = Beta<NS / 2>;
         const BH bl = half<C, 0>(chv, 0, ln);
@@ -378,6 +398,41 @@ __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs
             lo = (uint64_t)(bl ^ br) | ((uint64_t)br << (NS / 2));
         }
     }
+#else
+    // Stage LOG_N-1 held in VGPRs; the channel is read once per half (the second read is
+    // served by the caches) and is never live across a half's subtree.
+#if PL_SC_STAMPS
+    uint64_t st1 = st0;
+#endif
+    {
+        using BH = Beta<NS / 2>;
+        constexpr int E = NS / 2;
+        BH bl = 0, br = 0;
+        if constexpr (nt<C>(C::LOG_N - 1, 0) != R0) {
+            float a[E];
+#pragma unroll
+            for (int j = 0; j < E; ++j) a[j] = fop<C::FM>(-ch[j * G + res], -ch[(j + E) * G + res], lmax);
+            if constexpr (E == 1) bl = lnode<C, C::LOG_N - 1, 0>(a[0], ln);
+            else bl = node<C, C::LOG_N - 1, 0>(a, ln);
+        }
+        {
+            const float* chp = ch;
+            asm volatile("" : "+v"(chp) : "v"(bl));
+            float a[E];
+#pragma unroll
+            for (int j = 0; j < E; ++j)
+                a[j] = gop(-chp[j * G + res], -chp[(j + E) * G + res], (uint32_t)(bl >> j) << 31);
+            if constexpr (E == 1) br = lnode<C, C::LOG_N - 1, N / 2>(a[0], ln);
+            else br = node<C, C::LOG_N - 1, N / 2>(a, ln);
+        }
+        if constexpr (NS / 2 >= 64) {
+            lo = (uint64_t)(bl ^ br);
+            hi = (uint64_t)br;
+        } else {
+            lo = (uint64_t)(bl ^ br) | ((uint64_t)br << (NS / 2));
+        }
+    }
+#endif
     // u = x * G_n (G_n is an involution): in-lane spans on the packed slots, then the
     // cross-lane spans with the mirror DPP (the low element of each pair takes the XOR).
     {
@@ -403,43 +458,88 @@ __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs
 #pragma unroll
         for (int i = 0; i < WPL; ++i) mine[i] = w[i];
     }
+#if PL_SC_STAMPS
+    uint64_t st2 = __builtin_amdgcn_s_memtime();
+#endif
     __syncthreads();
+#if PL_SC_STAMPS
+    uint64_t st3 = __builtin_amdgcn_s_memtime();
+#endif
     // Information bits (info_pos ascending, polar_sc.py:127) -> coalesced rows.
     // info_loc[m] = (lane-in-group << 8) | slot of the m-th information position.
     const uint32_t* ubase = ulds + wave * 64 * WPL;
-    for (int m = lane; m < k; m += 64) {
-        const int loc = info_loc[m];
-        const int l = loc >> 8, slot = loc & 255;
-        const uint32_t* src = ubase + l * WPL + (slot >> 5);
-        const int sh = slot & 31;
+    if (OUT == OUT_F32 && (k & 3) == 0 && ((reinterpret_cast<uintptr_t>(out) & 15) == 0)) {
+        // 16-byte stores: lane writes info bits 4c..4c+3 of a row (1 KiB per wave-instruction)
+        const int kq = k >> 2;
+        for (int c = lane; c < kq; c += 64) {
+            const int4 l4 = reinterpret_cast<const int4*>(info_loc)[c];
+            const int lc[4] = {l4.x, l4.y, l4.z, l4.w};
+            int off[4], sh[4];
 #pragma unroll
-        for (int g = 0; g < CW; ++g) {
-            const int64_t row = cw0 + g;
-            if (row < bs) {
-                const uint32_t bit = (src[g * G * WPL] >> sh) & 1u;
-                if constexpr (OUT == OUT_F32) {
-                    static_cast<float*>(out)[row * k + m] = bit ? 1.0f : 0.0f;
-                } else {
-                    static_cast<uint8_t*>(out)[row * k + m] = (uint8_t)bit;
+            for (int i = 0; i < 4; ++i) {
+                off[i] = (lc[i] >> 8) * WPL + ((lc[i] & 255) >> 5);
+                sh[i] = lc[i] & 31;
+            }
+#pragma unroll
+            for (int g = 0; g < CW; ++g) {
+                const int64_t row = cw0 + g;
+                if (row < bs) {
+                    const uint32_t* src = ubase + g * G * WPL;
+                    float4 v;
+                    v.x = (float)((src[off[0]] >> sh[0]) & 1u);
+                    v.y = (float)((src[off[1]] >> sh[1]) & 1u);
+                    v.z = (float)((src[off[2]] >> sh[2]) & 1u);
+                    v.w = (float)((src[off[3]] >> sh[3]) & 1u);
+                    reinterpret_cast<float4*>(static_cast<float*>(out) + row * k)[c] = v;
+                }
+            }
+        }
+    } else {
+        for (int m = lane; m < k; m += 64) {
+            const int loc = info_loc[m];
+            const int l = loc >> 8, slot = loc & 255;
+            const uint32_t* src = ubase + l * WPL + (slot >> 5);
+            const int sh = slot & 31;
+#pragma unroll
+            for (int g = 0; g < CW; ++g) {
+                const int64_t row = cw0 + g;
+                if (row < bs) {
+                    const uint32_t bit = (src[g * G * WPL] >> sh) & 1u;
+                    if constexpr (OUT == OUT_F32) {
+                        static_cast<float*>(out)[row * k + m] = bit ? 1.0f : 0.0f;
+                    } else {
+                        static_cast<uint8_t*>(out)[row * k + m] = (uint8_t)bit;
+                    }
                 }
             }
         }
     }
+#if PL_SC_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+    uint64_t st4 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) {
+        uint64_t* d = reinterpret_cast<uint64_t*>(static_cast<float*>(out) + bs * k) + (blockIdx.x * kWaves + wave) * 8;
+        d[0] = st0; d[1] = st1; d[2] = st2; d[3] = st3; d[4] = st4;
+        d[5] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));  // HW_REG_HW_ID (placement)
+    }
+#endif
 }
 
 }  // namespace pls
 
 // Entry points instantiated per code: the including translation unit defines PlCode first.
 #define PL_SC_STATIC_KERNELS(CODE)                                                                           \
-    extern "C" __global__ __launch_bounds__(64 * pls::kWaves, 2) void pl_sc_static_f32(                      \
+    extern "C" __global__ __launch_bounds__(64 * pls::kWaves, PL_SC_MINW) void pl_sc_static_f32(                      \
         const float* __restrict__ llr, int64_t bs, void* __restrict__ out, const int32_t* __restrict__ info_loc, \
-        int k, float lmax) {                                                                                 \
+        int k, float lmax) {                                                                                  \
         __shared__ uint32_t ulds[pls::kWaves * 64 * ((CODE::NS + 31) / 32)];                                 \
-        pls::decode<CODE, pls::OUT_F32>(llr, bs, out, info_loc, k, lmax, ulds);                               \
+        pls::decode<CODE, pls::OUT_F32>(llr, bs, out, info_loc, k, lmax, ulds);               \
     }                                                                                                        \
-    extern "C" __global__ __launch_bounds__(64 * pls::kWaves, 2) void pl_sc_static_u8(                       \
+    extern "C" __global__ __launch_bounds__(64 * pls::kWaves, PL_SC_MINW) void pl_sc_static_u8(                       \
         const float* __restrict__ llr, int64_t bs, void* __restrict__ out, const int32_t* __restrict__ info_loc, \
-        int k, float lmax) {                                                                                 \
+        int k, float lmax) {                                                                                  \
         __shared__ uint32_t ulds[pls::kWaves * 64 * ((CODE::NS + 31) / 32)];                                 \
-        pls::decode<CODE, pls::OUT_U8>(llr, bs, out, info_loc, k, lmax, ulds);                                \
+        pls::decode<CODE, pls::OUT_U8>(llr, bs, out, info_loc, k, lmax, ulds);                \
     }
+
+#endif  // PL_SC_STATIC_H

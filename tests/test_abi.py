@@ -63,3 +63,35 @@ def test_no_cpu_fallback_without_gpu():
     dec = polar_amd.SC_Dec(torch.arange(32), 64)
     with pytest.raises(RuntimeError):
         dec(torch.zeros(2, 64))
+
+
+def test_specialised_kernel_compiles_without_gpu(tmp_path):
+    """pl_sc_specialize runs hiprtc only (no HIP device): the code object lands in the cache dir
+    and carries both entry points for gfx950."""
+    import numpy as np
+    from polar_amd import _lib
+    L = _lib.lib()
+    mask = np.zeros(32, dtype=np.uint8)
+    mask[[0, 1, 2, 4, 8, 16, 3, 5, 6, 9, 10, 12]] = 1
+    buf = ctypes.create_string_buffer(4096)
+    rc = L.pl_sc_specialize(32, mask.ctypes.data_as(ctypes.c_void_p), 0, str(tmp_path).encode(), buf, 4096)
+    assert rc == 0, L.pl_last_error_string()
+    path = buf.value.decode()
+    assert path.startswith(str(tmp_path)) and os.path.exists(path)
+    blob = open(path, "rb").read()
+    assert b"pl_sc_static_f32" in blob and b"pl_sc_static_u8" in blob and b"gfx950" in blob
+    # content-addressed: the same code maps to the same file, a different one to another
+    buf2 = ctypes.create_string_buffer(4096)
+    assert L.pl_sc_specialize(32, mask.ctypes.data_as(ctypes.c_void_p), 0, str(tmp_path).encode(), buf2, 4096) == 0
+    assert buf2.value == buf.value
+    mask[31] = 1
+    assert L.pl_sc_specialize(32, mask.ctypes.data_as(ctypes.c_void_p), 0, str(tmp_path).encode(), buf2, 4096) == 0
+    assert buf2.value != buf.value
+
+
+def test_reference_codes_are_prebuilt():
+    """build() pre-compiles the specialised kernels of every pinned reference code."""
+    from polar_amd import build as b
+    if not os.path.isdir(b.KCACHE):
+        pytest.fail("polar_amd/kcache missing (run __graft_entry__.build())")
+    assert len([f for f in os.listdir(b.KCACHE) if f.endswith(".co")]) >= len(b.reference_codes())

@@ -5,6 +5,8 @@
   * full-size (512,1024) x 65536 batch: noiseless encode->decode round trip + oracle on a sample
   * edge cases: bs = 0 / 1 / ragged, k = 0 / n, exact zeros, saturation, uint8 output, CPU input
   * exact-boxplus mode: statistical gate (see tests/test_oracle.py for why)
+Both SC kernels are held to the same bar: the code-specialised one (default; pre-built for the
+reference codes, compiled with hiprtc at plan time for any other code) and the generic one.
 """
 import glob
 import os
@@ -26,20 +28,27 @@ def pa():
     return polar_amd
 
 
-def _plan(pa, fp, n, f_mode=0, L=1):
+KINDS = ("specialized", "generic")
+
+
+def _plan(pa, fp, n, f_mode=0, L=1, kind="specialized"):
     from polar_amd import _lib
-    return _lib.Plan(n, pa.frozen_mask(fp, n), L, f_mode)
+    flags = _lib.PL_PLAN_GENERIC if kind == "generic" else 0
+    plan = _lib.Plan(n, pa.frozen_mask(fp, n), L, f_mode, flags=flags)
+    assert plan.kernel()[0] == kind, plan.kernel()
+    return plan
 
 
 def _sets(d):
     return [k[4:] for k in d.files if k.startswith("llr_")]
 
 
+@pytest.mark.parametrize("kind", KINDS)
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "sc_*.npz"))), ids=os.path.basename)
-def test_sc_golden_bit_exact(pa, path):
+def test_sc_golden_bit_exact(pa, path, kind):
     d = np.load(path)
     n = int(d["n"])
-    plan = _plan(pa, d["frozen_pos"], n)
+    plan = _plan(pa, d["frozen_pos"], n, kind=kind)
     for name in _sets(d):
         x = torch.from_numpy(d["llr_" + name]).cuda()
         bits = pa.ops.sc_decode(plan, x)
@@ -48,9 +57,12 @@ def test_sc_golden_bit_exact(pa, path):
         assert np.array_equal(got, d["bits_" + name]), f"{name}: {int((got != d['bits_' + name]).any(1).sum())} rows differ"
 
 
+@pytest.mark.parametrize("kind", KINDS)
 @pytest.mark.parametrize("log_n", list(range(1, 12)))
 @pytest.mark.parametrize("rate", [0.25, 0.5, 0.75])
-def test_sc_random_vs_oracle(pa, log_n, rate):
+def test_sc_random_vs_oracle(pa, log_n, rate, kind):
+    if kind == "specialized" and log_n > 8:
+        pytest.skip("hiprtc compile per random code; large n covered by the reference codes")
     n = 1 << log_n
     rng = np.random.default_rng(log_n * 10 + int(rate * 4))
     k = max(1, int(n * rate))
@@ -59,14 +71,15 @@ def test_sc_random_vs_oracle(pa, log_n, rate):
     llr = (rng.standard_normal((bs, n)) * 3).astype(np.float32)
     llr[rng.random((bs, n)) < 0.05] = 0.0
     want = oracle.sc_decode(llr, fp)
-    plan = _plan(pa, fp, n)
+    plan = _plan(pa, fp, n, kind=kind)
     got = pa.ops.sc_decode(plan, torch.from_numpy(llr).cuda()).cpu().numpy()
     assert np.array_equal(got, want)
     got8 = pa.ops.sc_decode(plan, torch.from_numpy(llr).cuda(), out_dtype=torch.uint8).cpu().numpy()
     assert np.array_equal(got8, want.astype(np.uint8))
 
 
-def test_sc_reference_frozen_all_shapes(pa):
+@pytest.mark.parametrize("kind", KINDS)
+def test_sc_reference_frozen_all_shapes(pa, kind):
     fs = np.load(os.path.join(GOLDEN, "frozen_sets.npz"))
     rng = np.random.default_rng(5)
     for key in fs.files:
@@ -75,8 +88,13 @@ def test_sc_reference_frozen_all_shapes(pa):
             continue
         fp = fs[key]
         llr = (rng.standard_normal((129, n)) * 2 + 0.5).astype(np.float32)
-        got = pa.ops.sc_decode(_plan(pa, fp, n), torch.from_numpy(llr).cuda()).cpu().numpy()
+        got = pa.ops.sc_decode(_plan(pa, fp, n, kind=kind), torch.from_numpy(llr).cuda()).cpu().numpy()
         assert np.array_equal(got, oracle.sc_decode(llr, fp)), key
+        # ties, exact zeros and saturation: every shortcut's fallback path
+        t = (np.round(rng.standard_normal((129, n)) * 2) * 0.5).astype(np.float32)
+        t[:, ::5] *= 100.0
+        got = pa.ops.sc_decode(_plan(pa, fp, n, kind=kind), torch.from_numpy(t).cuda()).cpu().numpy()
+        assert np.array_equal(got, oracle.sc_decode(t, fp)), key
 
 
 def test_sc_full_batch_roundtrip_and_sample(pa):
@@ -136,13 +154,34 @@ def test_sc_dropin_module_matches_reference_contract(pa):
     assert dec(x.cuda()).device.type == "cuda"
 
 
-def test_sc_exact_mode_statistical(pa):
+@pytest.mark.parametrize("kind", KINDS)
+def test_sc_exact_mode_statistical(pa, kind):
     for path in sorted(glob.glob(os.path.join(GOLDEN, "sc_*.npz"))):
         d = np.load(path)
-        plan = _plan(pa, d["frozen_pos"], int(d["n"]), f_mode=1)
+        plan = _plan(pa, d["frozen_pos"], int(d["n"]), f_mode=1, kind=kind)
         for name in _sets(d):
             if not name.startswith("awgn"):
                 continue
             got = pa.ops.sc_decode(plan, torch.from_numpy(d["llr_" + name]).cuda()).cpu().numpy().astype(np.uint8)
             rate = float((got != d["exact_" + name]).any(1).mean())
             assert rate <= 0.02, (path, name, rate)
+
+
+def test_sc_specialized_jit_for_an_arbitrary_code(pa, tmp_path, monkeypatch):
+    """A code with no pre-built kernel: compiled by hiprtc at plan creation, cached, bit-exact."""
+    from polar_amd import _lib
+    monkeypatch.setenv("PL_KERNEL_CACHE", str(tmp_path))
+    rng = np.random.default_rng(77)
+    n = 1024
+    fp = np.sort(rng.permutation(n)[:400])
+    plan = _lib.Plan(n, pa.frozen_mask(fp, n), 1, 0)
+    kind, path = plan.kernel()
+    assert kind == "specialized" and path.startswith(str(tmp_path)), (kind, path)
+    llr = (rng.standard_normal((4099, n)) * 2.5).astype(np.float32)
+    llr[:, ::11] = np.round(llr[:, ::11])
+    got = pa.ops.sc_decode(plan, torch.from_numpy(llr).cuda()).cpu().numpy()
+    assert np.array_equal(got, oracle.sc_decode(llr, fp))
+    # second plan for the same code: cache hit, same file; cache-only plans never compile
+    assert _lib.Plan(n, pa.frozen_mask(fp, n), 1, 0, flags=_lib.PL_PLAN_CACHE_ONLY).kernel() == (kind, path)
+    fp2 = np.sort(rng.permutation(n)[:401])
+    assert _lib.Plan(n, pa.frozen_mask(fp2, n), 1, 0, flags=_lib.PL_PLAN_CACHE_ONLY).kernel()[0] == "generic"

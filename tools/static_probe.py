@@ -56,10 +56,10 @@ def build(k, n, name, flags):
     os.makedirs(OUT, exist_ok=True)
     src = os.path.join(OUT, f"st_{name}.hip")
     open(src, "w").write('#include "sc_static.h"\n' + code_src(mask) + "PL_SC_STATIC_KERNELS(PlCode)\n" + r'''
-extern "C" int st_launch(const float* llr, long bs, void* out, const int* info_loc, int k, float lmax, void* st) {
+extern "C" int st_launch(const float* llr, long bs, void* out, const int* info_loc, int k, float lmax, void* st, long pf) {
     const long per = (long)pls::kWaves * (64 / PlCode::G);
     hipLaunchKernelGGL(pl_sc_static_f32, dim3((unsigned)((bs + per - 1) / per)), dim3(64 * pls::kWaves), 0,
-                       (hipStream_t)st, llr, (int64_t)bs, out, info_loc, k, lmax);
+                       (hipStream_t)st, llr, (int64_t)bs, out, info_loc, k, lmax, (int64_t)pf);
     return (int)hipGetLastError();
 }
 ''')
@@ -97,19 +97,36 @@ def run(k, n, names):
     print(f"library kernel ({k},{n}) bs={bs}: {t_ref:.4f} ms  {bs / t_ref / 1e3:.1f} Mcw/s", flush=True)
     for name in names:
         L = ctypes.CDLL(os.path.join(OUT, f"st_{name}.so"))
-        L.st_launch.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_void_p]
+        L.st_launch.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_long]
+        pfs = [int(v) for v in os.environ.get("PROBE_PF", "0").split(",")]
+        if "stamp" in name:
+            nw = (bs // (64 // (1 << lg_of(n))))
+            big = torch.zeros(bs * k + nw * 16 + 64, device=dev)
+            L.st_launch(llr.data_ptr(), bs, big.data_ptr(), iloc.data_ptr(), k, 30.0, st, 0)
+            L.st_launch(llr.data_ptr(), bs, big.data_ptr(), iloc.data_ptr(), k, 30.0, st, 0)
+            torch.cuda.synchronize()
+            d = big[bs * k: bs * k + nw * 16].view(torch.int64).view(nw, 8).cpu().numpy()
+            t0 = d[:, 0].min()
+            ld, tree, bar, outp = d[:, 1] - d[:, 0], d[:, 2] - d[:, 1], d[:, 3] - d[:, 2], d[:, 4] - d[:, 3]
+            tot = d[:, 4] - d[:, 0]
+            for nm, v in (("load", ld), ("tree", tree), ("barrier", bar), ("output", outp), ("total", tot)):
+                print(f"  stamp {nm}: mean {v.mean():.0f} p10 {np.percentile(v, 10):.0f} p50 {np.median(v):.0f} p90 {np.percentile(v, 90):.0f}")
+            print(f"  span {d[:, 4].max() - t0}  start spread p50 {np.median(d[:, 0] - t0):.0f} p90 {np.percentile(d[:, 0] - t0, 90):.0f}")
+            np.save(os.path.join(ROOT, "gpurun_out", f"stamps_{name}.npy"), d)
+            continue
         out = torch.empty((bs, k), device=dev)
         ok = True
         for x in (llr, x2, x3):
             want = ops.sc_decode(plan, x)
             out.fill_(7)
-            assert L.st_launch(x.data_ptr(), bs, out.data_ptr(), iloc.data_ptr(), k, 30.0, st) == 0
+            assert L.st_launch(x.data_ptr(), bs, out.data_ptr(), iloc.data_ptr(), k, 30.0, st, pfs[-1]) == 0
             torch.cuda.synchronize()
             nbad = int((out != want).any(dim=1).sum())
             ok &= nbad == 0
             if nbad: print(f"  {name}: {nbad} mismatching rows", flush=True)
-        t = tm(lambda: L.st_launch(llr.data_ptr(), bs, out.data_ptr(), iloc.data_ptr(), k, 30.0, st))
-        print(f"static[{name}] ({k},{n}): {t:.4f} ms  {bs / t / 1e3:.1f} Mcw/s  exact={ok}", flush=True)
+        for pf in pfs:
+            t = tm(lambda: L.st_launch(llr.data_ptr(), bs, out.data_ptr(), iloc.data_ptr(), k, 30.0, st, pf))
+            print(f"static[{name}] pf={pf} ({k},{n}): {t:.4f} ms  {bs / t / 1e3:.1f} Mcw/s  exact={ok}", flush=True)
 
 if __name__ == "__main__":
     if sys.argv[1] == "build":
