@@ -174,6 +174,7 @@ def main():
             "config": {"workload": f"{a.decoder.upper()} decode (k={k}, n={n}), bs={bs} per GPU"
                                    + (f", L={L}" if L > 1 else ""),
                        "k": k, "n": n, "bs_per_gpu": bs, "global_batch": bs * world,
+                       "kernel": plan.kernel()[0] if a.decoder == "sc" else "scl",
                        "parallelism": f"dp{world}"},
             "info_gbit_s": round(total_cw * k / wall / 1e9, 4),
             "bler": round(float(blk[0].item()) / float(blk[1].item()), 6),
