@@ -34,8 +34,10 @@ REF_BLER_2DB = 0.9999  # reference x_run SC BLER at (512,1024),
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default 1000 SC / 20 SCL)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed steps (default 200 SC / 3 SCL)")
+    ap.add_argument("--settle-ms", type=float, default=100.0,
+                    help="untimed launches before the warmup steps so the GPU clock leaves its idle state")
     ap.add_argument("--k", type=int, default=512)
     ap.add_argument("--n", type=int, default=1024)
     ap.add_argument("--bs", type=int, default=65536, help="codewords per GPU")
@@ -44,7 +46,12 @@ def parse():
     ap.add_argument("--list-size", type=int, default=8)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.steps is None:
+        a.steps = 1000 if a.decoder == "sc" else 20
+    if a.warmup is None:
+        a.warmup = 200 if a.decoder == "sc" else 3
+    return a
 
 
 def cpu_baseline(llr_host, fp, k, n, decoder, L, budget_s):
@@ -123,6 +130,13 @@ def main():
         else:
             ops.scl_decode(plan, llr, out=out)
 
+    # DVFS: a cold MI355X runs the first few ms of work at a lower clock (measured: 0.127 ms/launch
+    # with 3 warmup steps vs 0.119 ms after ~0.1 s of load), so settle the clock first.
+    t_settle = time.perf_counter()
+    while (time.perf_counter() - t_settle) * 1e3 < a.settle_ms:
+        for _ in range(50):
+            step()
+        torch.cuda.synchronize(dev)
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize(dev)

@@ -95,11 +95,11 @@ def _specialize_one(args):
     buf = ctypes.create_string_buffer(4096)
     rc = L.pl_sc_specialize(n, mask_bytes, f_mode, KCACHE.encode(), buf, 4096)
     if rc != 0:
-        return f"n={n} f_mode={f_mode}: {L.pl_last_error_string().decode(errors='replace')[:500]}"
-    return None
+        return False, f"n={n} f_mode={f_mode}: {L.pl_last_error_string().decode(errors='replace')[:500]}"
+    return True, os.path.basename(buf.value.decode())
 
 
-def prebuild_codes(codes, workers=None):
+def prebuild_codes(codes, workers=None, prune=True):
     """Compile the specialised SC kernels of `codes` = [(frozen_mask uint8[n], f_mode)] into
     KCACHE (content-addressed: unchanged codes are found and skipped)."""
     os.makedirs(KCACHE, exist_ok=True)
@@ -107,9 +107,15 @@ def prebuild_codes(codes, workers=None):
     jobs.sort(key=lambda j: -j[0])  # longest compiles first
     workers = workers or min(8, os.cpu_count() or 1)
     with ProcessPoolExecutor(max_workers=workers) as ex:
-        errs = [e for e in ex.map(_specialize_one, jobs) if e]
+        res = list(ex.map(_specialize_one, jobs))
+    errs = [v for ok, v in res if not ok]
     if errs:
         raise RuntimeError("specialised SC kernel pre-build failed:\n" + "\n".join(errs))
+    if prune:  # drop code objects of older kernel versions (they would only travel as dead weight)
+        keep = {v for ok, v in res if ok}
+        for f in os.listdir(KCACHE):
+            if f.endswith(".co") and f not in keep:
+                os.remove(os.path.join(KCACHE, f))
 
 
 def reference_codes():

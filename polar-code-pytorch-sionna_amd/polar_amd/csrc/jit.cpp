@@ -140,7 +140,23 @@ std::string static_source(int n, const uint8_t* frozen, int f_mode) {
     const int log_n = log2_exact(n), lg = static_log_g(log_n);
     const std::vector<uint8_t> nt = node_types(n, frozen);
     std::ostringstream o;
-    o << kStaticSrc << "\nstruct PlCode {\n  static constexpr int N = " << n << ", LOG_N = " << log_n
+    // PL_SC_DEFINES="NAME=VALUE ..." overrides the kernel's tuning macros (development variants;
+    // part of the source, hence of the cache key)
+    if (const char* defs = getenv("PL_SC_DEFINES")) {
+        std::istringstream in(defs);
+        std::string tok;
+        while (in >> tok) {
+            const size_t eq = tok.find('=');
+            o << "#define " << tok.substr(0, eq) << " " << (eq == std::string::npos ? "1" : tok.substr(eq + 1)) << "\n";
+        }
+    }
+    // PL_SC_SOURCE=<file> replaces the embedded sc_static.h (development A/B of kernel versions)
+    std::string body = kStaticSrc;
+    if (const char* alt = getenv("PL_SC_SOURCE")) {
+        std::vector<char> text;
+        if (*alt && read_file(alt, text)) body.assign(text.begin(), text.end());
+    }
+    o << body << "\nstruct PlCode {\n  static constexpr int N = " << n << ", LOG_N = " << log_n
       << ", LOG_G = " << lg << ", G = " << (1 << lg) << ", NS = " << (n >> lg) << ", FM = " << f_mode
       << ";\n  static constexpr unsigned char NT[" << nt.size() << "] = {";
     for (size_t i = 0; i < nt.size(); ++i) o << (i ? "," : "") << (int)nt[i];

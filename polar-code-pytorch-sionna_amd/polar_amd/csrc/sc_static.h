@@ -45,6 +45,35 @@ typedef unsigned long long uint64_t;
 typedef unsigned long uintptr_t;
 #endif
 
+// Tuning macros (overridable per build; PL_SC_DEFINES in jit.cpp for A/B variants)
+#ifndef PL_SC_F_BITOP3
+#define PL_SC_F_BITOP3 0  // A/B on MI355X: 1 (explicit v_bitop3 sign merge) was slower
+#endif
+#ifndef PL_SC_BIT31_ASM
+#define PL_SC_BIT31_ASM 0  // 1: opaque shift (no v_mul_lo fusion); measured slower overall
+#endif
+#ifndef PL_SC_SPC_BALLOT
+#define PL_SC_SPC_BALLOT 0  // 1: SALU ballot uniqueness test instead of a DPP count; measured slower
+#endif
+#ifndef PL_SC_ROOT_MODE
+#define PL_SC_ROOT_MODE 0
+#endif
+#ifndef PL_SC_MINW
+#define PL_SC_MINW 2
+#endif
+#ifndef PL_SC_STAMPS
+#define PL_SC_STAMPS 0
+#endif
+#ifndef PL_SC_DIAG_SKIP_LANE
+#define PL_SC_DIAG_SKIP_LANE 0
+#endif
+#ifndef PL_SC_DIAG_SKIP_SPECIAL
+#define PL_SC_DIAG_SKIP_SPECIAL 0
+#endif
+#ifndef PL_SC_PERSIST
+#define PL_SC_PERSIST 0  // 1: persistent software-pipelined waves (grid = resident waves)
+#endif
+
 namespace pls {
 
 enum : int { R0 = 0, R1 = 1, REP = 2, SPC = 3, GEN = 4 };
@@ -93,7 +122,12 @@ template <int FM>
 __device__ __forceinline__ float fop(float x, float y, float lmax) {
     if constexpr (FM == 0) {
         const float m = fminf(fminf(fabsf(x), fabsf(y)), lmax);
+#if PL_SC_F_BITOP3
+        // m | ((x ^ y) & sign): v_min3 + v_xor + v_bitop3 ((S0 & S1) | S2, table 0xEA)
+        return uf(__builtin_amdgcn_bitop3_b32(fu(x) ^ fu(y), 0x80000000u, fu(m), 0xEA));
+#else
         return uf(fu(m) | ((fu(x) ^ fu(y)) & 0x80000000u));
+#endif
     } else {
         const float xc = fminf(fmaxf(x, -lmax), lmax), yc = fminf(fmaxf(y, -lmax), lmax);
         float o = logf(1.0f + expf(xc + yc));
@@ -101,9 +135,24 @@ __device__ __forceinline__ float fop(float x, float y, float lmax) {
         return o;
     }
 }
-// g with the sign flip given as a mask (0 or 0x80000000): (1-2u)x + y, one rounding.
-__device__ __forceinline__ float gop(float x, float y, uint32_t sgn) { return uf(fu(x) ^ sgn) + y; }
-// hard decision of a leaf: u = 1 iff !(llr > 0)  (polar_sc.py:94-97)
+// g, polar_sc.py:49-53: (1-2u)x + y == (u ? -x : x) + y, one rounding.  The flip is the sign
+// bit (bit 31) of t; bitop3 S1 ^ (S0 & S2) (table 0x6c) applies it in one op.
+__device__ __forceinline__ float flip31(float x, uint32_t t) {
+    return uf(__builtin_amdgcn_bitop3_b32(t, fu(x), 0x80000000u, 0x6c));
+}
+__device__ __forceinline__ float gop(float x, float y, uint32_t t) { return flip31(x, t) + y; }
+// bit j of packed partial sums w moved to bit 31 with one shift (lower bits are don't-care for
+// flip31); j is a compile-time constant after unrolling
+template <typename W>
+__device__ __forceinline__ uint32_t bit31(W w, int j) {
+    uint32_t t = j <= 31 ? (uint32_t)(w << (31 - j)) : (uint32_t)(w >> (j - 31));
+#if PL_SC_BIT31_ASM
+    asm("" : "+v"(t));  // keep it one v_lshlrev (only bit 31 is demanded: LLVM would fuse shifts into v_mul_lo)
+#endif
+    return t;
+}
+// hard decision of a leaf, u = 1 iff !(llr > 0) (polar_sc.py:94-97), as a bit-31 flag
+__device__ __forceinline__ uint32_t hd31(float x) { return (x > 0.0f) ? 0u : 0x80000000u; }
 __device__ __forceinline__ uint32_t hd(float x) { return (x > 0.0f) ? 0u : 1u; }
 
 struct Lane {
@@ -129,8 +178,22 @@ __device__ __forceinline__ float grp_sumf(float v) {
     if constexpr (LG >= 1) v = v + mirf<2>(v);
     return v;
 }
+// wave mask with the lowest lane of every aligned S-lane block set
+template <int S>
+__device__ __forceinline__ constexpr uint64_t blocklow() {
+    return S == 1 ? ~0ull : S == 2 ? 0x5555555555555555ull : S == 4 ? 0x1111111111111111ull
+         : S == 8 ? 0x0101010101010101ull : 0x0001000100010001ull;
+}
+// True if some S-lane block whose lanes are set in `live` has two or more lanes set in `m`
+// (m must have at least one lane set in every block): subtracting 1 per block clears each
+// block's lowest set lane without borrowing across blocks.
+template <int S>
+__device__ __forceinline__ bool multi_in_block(uint64_t m, uint64_t live) {
+    return ((m & (m - blocklow<S>())) & live) != 0;
+}
 
 // ---------------- lane-level nodes: size 2^s <= G, one (replicated) LLR per lane ----------
+// Partial sums are returned as bit-31 flags (0 / 0x80000000) so g consumes them directly.
 template <class C, int s, int P>
 __device__ uint32_t lnode(float a, const Lane& ln);
 
@@ -141,8 +204,10 @@ __device__ __forceinline__ uint32_t lsplit(float a, const Lane& ln) {
     const uint32_t L = ln.lom[s];
     uint32_t bl = 0;
     if constexpr (nt<C>(s - 1, P) != R0) bl = lnode<C, s - 1, P>(fop<C::FM>(a, y, ln.lmax), ln);
-    const uint32_t m = bl << 31;
-    const float x = uf(fu(a) ^ (m & L)) + uf(fu(y) ^ (m & ~L));
+    // both lanes of the pair evaluate (1-2u) alpha_lo + alpha_hi: the low lane flips its own
+    // value, the high lane its partner's (bitop3 S1 ^ (S0 & S2) / S1 ^ (S0 & ~S2))
+    const float x = uf(__builtin_amdgcn_bitop3_b32(bl, fu(a), L, 0x6c)) +
+                    uf(__builtin_amdgcn_bitop3_b32(bl, fu(y), L, 0x9c));
     const uint32_t br = lnode<C, s - 1, P + S / 2>(x, ln);
     return br ^ (bl & L);
 }
@@ -150,23 +215,27 @@ __device__ __forceinline__ uint32_t lsplit(float a, const Lane& ln) {
 template <class C, int s, int P>
 __device__ __forceinline__ uint32_t lnode(float a, const Lane& ln) {
     constexpr int T = nt<C>(s, P);
+#if PL_SC_DIAG_SKIP_LANE
+    if constexpr (s == C::LOG_G) return hd31(a);  // diagnostic only: timing without the lane-level subtrees
+#endif
     if constexpr (T == R0) {
         return 0u;
     } else if constexpr (s == 0) {
-        return hd(a);
+        return hd31(a);
     } else if constexpr (T == REP) {
         float v = a;
         if constexpr (s >= 4) v = v + mirf<16>(v);
         if constexpr (s >= 3) v = v + mirf<8>(v);
         if constexpr (s >= 2) v = v + mirf<4>(v);
         v = v + mirf<2>(v);
-        return hd(v);
+        return hd31(v);
     } else if constexpr (T == R1 && C::FM == 0) {
-        if (!__any(a == 0.0f)) return fu(a) >> 31;
+        if (!__any(a == 0.0f)) return fu(a) & 0x80000000u;
         return lsplit<C, s, P>(a, ln);
     } else if constexpr (T == SPC && C::FM == 0) {
         // magnitudes compared as integers (non-negative floats order like their bit patterns)
-        const uint32_t b = fu(a) >> 31;
+        constexpr int S = 1 << s;
+        const uint32_t b = fu(a) & 0x80000000u;
         const uint32_t ab = fu(a) & 0x7FFFFFFFu;
         uint32_t par = b, mn = ab;
         if constexpr (s >= 4) { par ^= mir<16>(par); mn = min(mn, mir<16>(mn)); }
@@ -174,14 +243,19 @@ __device__ __forceinline__ uint32_t lnode(float a, const Lane& ln) {
         if constexpr (s >= 2) { par ^= mir<4>(par); mn = min(mn, mir<4>(mn)); }
         par ^= mir<2>(par);
         mn = min(mn, mir<2>(mn));
-        const uint32_t eq = (ab == mn) ? 1u : 0u;
-        uint32_t cnt = eq;
+        const bool eq = ab == mn;
+#if PL_SC_SPC_BALLOT
+        const bool bad_lane = (ab == 0u) | ((par != 0u) & (mn >= fu(ln.lmax)));
+        const bool bad = __any(bad_lane) || multi_in_block<S>(__ballot(eq), __ballot(par != 0u));
+#else
+        uint32_t cnt = eq ? 1u : 0u;
         if constexpr (s >= 4) cnt += mir<16>(cnt);
         if constexpr (s >= 3) cnt += mir<8>(cnt);
         if constexpr (s >= 2) cnt += mir<4>(cnt);
         cnt += mir<2>(cnt);
-        const bool bad = (ab == 0u) | ((par != 0u) & ((cnt != 1u) | (mn >= fu(ln.lmax))));
-        if (!__any(bad)) return b ^ (par & eq);
+        const bool bad = __any((ab == 0u) | ((par != 0u) & ((cnt != 1u) | (mn >= fu(ln.lmax)))));
+#endif
+        if (!bad) return b ^ (eq ? par : 0u);
         return lsplit<C, s, P>(a, ln);
     } else {
         return lsplit<C, s, P>(a, ln);
@@ -196,7 +270,7 @@ template <class C, int s, int P>
 __device__ __forceinline__ Beta<(1 << (s - 1)) / C::G> child(const float (&x)[(1 << (s - 1)) / C::G],
                                                              const Lane& ln) {
     if constexpr ((1 << (s - 1)) == C::G) {
-        return (Beta<1>)lnode<C, s - 1, P>(x[0], ln);
+        return (Beta<1>)(lnode<C, s - 1, P>(x[0], ln) >> 31);
     } else {
         return node<C, s - 1, P>(x, ln);
     }
@@ -214,7 +288,9 @@ __device__ __forceinline__ Beta<(1 << s) / C::G> split(const float (&a)[(1 << s)
         for (int j = 0; j < H; ++j) x[j] = fop<C::FM>(a[j], a[j + H], ln.lmax);
         bl = child<C, s, P>(x, ln);
 #pragma unroll
-        for (int j = 0; j < H; ++j) x[j] = gop(a[j], a[j + H], ((uint32_t)(bl >> j) << 31));
+        for (int j = 0; j < H; ++j) {
+            x[j] = gop(a[j], a[j + H], bit31(bl, j));
+        }
     } else {
 #pragma unroll
         for (int j = 0; j < H; ++j) x[j] = a[j] + a[j + H];
@@ -236,6 +312,9 @@ __device__ __forceinline__ Beta<(1 << s) / C::G> node(const float (&a)[(1 << s) 
     constexpr int E = (1 << s) / C::G;
     constexpr int T = nt<C>(s, P);
     using BT = Beta<E>;
+#if PL_SC_DIAG_SKIP_SPECIAL
+    if constexpr (T == REP || T == SPC || T == R1) return signs<C, E>(a);  // diagnostic only
+#endif
     if constexpr (T == R0) {
         return (BT)0;
     } else if constexpr (T == REP) {
@@ -268,10 +347,17 @@ __device__ __forceinline__ Beta<(1 << s) / C::G> node(const float (&a)[(1 << s) 
         BT eqm = 0;
 #pragma unroll
         for (int j = 0; j < E; ++j) eqm |= (BT)((fu(a[j]) & 0x7FFFFFFFu) == mn) << j;
+#if PL_SC_SPC_BALLOT
+        // unique minimum: no lane holds two, and no codeword group has two lanes holding one
+        const bool two = (eqm & (eqm - 1)) != 0;
+        const bool bad_lane = z | ((par != 0u) & (two | (mn >= fu(ln.lmax))));
+        const bool bad = __any(bad_lane) || multi_in_block<C::G>(__ballot(eqm != 0), __ballot(par != 0u));
+#else
         uint32_t cnt = (uint32_t)__popcll((unsigned long long)eqm);
         cnt = grp<C::LOG_G>(cnt, [](uint32_t u, uint32_t v) { return u + v; });
-        const bool bad = z | ((par != 0u) & ((cnt != 1u) | (mn >= fu(ln.lmax))));
-        if (!__any(bad)) return par ? (BT)(b ^ eqm) : b;
+        const bool bad = __any(z | ((par != 0u) & ((cnt != 1u) | (mn >= fu(ln.lmax)))));
+#endif
+        if (!bad) return par ? (BT)(b ^ eqm) : b;
         return split<C, s, P>(a, ln);
     } else {
         return split<C, s, P>(a, ln);
@@ -283,26 +369,39 @@ __device__ __forceinline__ Beta<(1 << s) / C::G> node(const float (&a)[(1 << s) 
 // stage LOG_N-1 buffers are "virtual": each of their LLRs is recomputed from two channel values
 // when a pass of the stage-(LOG_N-1) node reads it (f for the left half, g with the left half's
 // partial sums for the right), so the largest stage buffer never occupies registers.
+// f(-x,-y) = f(x,y) and g(-x,-y) = -g(x,y): the negation of polar_sc.py:122 costs nothing (the
+// sign of an exact zero is never observable: every decision treats +0 and -0 alike).
 template <class C>
 __device__ __forceinline__ float valpha(const float (&ch)[C::NS], int side, uint64_t blr, int j, float lmax) {
-    const float x = -ch[j], y = -ch[j + C::NS / 2];
-    return side == 0 ? fop<C::FM>(x, y, lmax) : gop(x, y, (uint32_t)(blr >> j) << 31);
+    const float x = ch[j], y = ch[j + C::NS / 2];
+    return side == 0 ? fop<C::FM>(x, y, lmax) : (-flip31(x, bit31(blr, j))) - y;
 }
 
-template <class C, int SIDE>
-__device__ __forceinline__ Beta<C::NS / 2> half(const float (&ch)[C::NS], uint64_t blr, const Lane& ln) {
+struct NoHook {
+    __device__ __forceinline__ void operator()() const {}
+};
+
+// `after` runs once the channel registers are dead (their last read is done): the pipelined
+// decoder refills them with the next batch's channel there.
+template <class C, int SIDE, class Hook = NoHook>
+__device__ __forceinline__ Beta<C::NS / 2> half(float (&ch)[C::NS], uint64_t blr, const Lane& ln,
+                                                const Hook& after = Hook()) {
     constexpr int s = C::LOG_N - 1, P = SIDE << s;
     constexpr int E = C::NS / 2;  // slots of the stage-(LOG_N-1) node per lane
     using BT = Beta<E>;
     constexpr int T = nt<C>(s, P);
     if constexpr (T == R0) {
+        after();
         return (BT)0;
     } else if constexpr (E == 1) {
-        return (BT)lnode<C, s, P>(valpha<C>(ch, SIDE, blr, 0, ln.lmax), ln);
+        const float a = valpha<C>(ch, SIDE, blr, 0, ln.lmax);
+        after();
+        return (BT)(lnode<C, s, P>(a, ln) >> 31);
     } else if constexpr (T != GEN) {
         float a[E];
 #pragma unroll
         for (int j = 0; j < E; ++j) a[j] = valpha<C>(ch, SIDE, blr, j, ln.lmax);
+        after();
         return node<C, s, P>(a, ln);
     } else {
         constexpr int H = E / 2, h = 1 << (s - 1);
@@ -319,7 +418,8 @@ __device__ __forceinline__ Beta<C::NS / 2> half(const float (&ch)[C::NS], uint64
 #pragma unroll
         for (int j = 0; j < H; ++j)
             x[j] = gop(valpha<C>(ch, SIDE, blr, j, ln.lmax), valpha<C>(ch, SIDE, blr, j + H, ln.lmax),
-                       (uint32_t)(bl >> j) << 31);
+                       bit31(bl, j));
+        after();
         const BH br = child<C, s, P + h>(x, ln);
         return (BT)(bl ^ br) | ((BT)br << H);
     }
@@ -345,129 +445,41 @@ __device__ __forceinline__ void lane_layout(int q, int& res, uint32_t (&lom)[5])
     }
 }
 
-#ifndef PL_SC_ROOT_MODE
-#define PL_SC_ROOT_MODE 0
-#endif
-#ifndef PL_SC_MINW
-#define PL_SC_MINW 2
-#endif
-#ifndef PL_SC_STAMPS
-#define PL_SC_STAMPS 0
-#endif
 
+// u = x * G_n (G_n is an involution): in-lane spans on the packed slots, then the cross-lane
+// spans with the mirror DPP (the low element of each pair takes the XOR).  Writes this lane's
+// u words to its LDS slot.
+template <class C>
+__device__ __forceinline__ void to_u(uint64_t lo, uint64_t hi, const Lane& ln, uint32_t* __restrict__ mine) {
+    constexpr int NS = C::NS, LG = C::LOG_G, WPL = (NS + 31) / 32;
+    constexpr uint64_t M[6] = {0x5555555555555555ull, 0x3333333333333333ull, 0x0f0f0f0f0f0f0f0full,
+                               0x00ff00ff00ff00ffull, 0x0000ffff0000ffffull, 0x00000000ffffffffull};
+#pragma unroll
+    for (int t = 0; t < 6; ++t) {
+        if ((1 << t) < NS) {
+            lo ^= (lo >> (1 << t)) & M[t];
+            hi ^= (hi >> (1 << t)) & M[t];
+        }
+    }
+    if constexpr (NS > 64) lo ^= hi;
+    uint32_t w[4] = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+#pragma unroll
+    for (int i = 0; i < WPL; ++i) {
+        if constexpr (LG >= 4) w[i] ^= mir<16>(w[i]) & ln.lom[4];
+        if constexpr (LG >= 3) w[i] ^= mir<8>(w[i]) & ln.lom[3];
+        if constexpr (LG >= 2) w[i] ^= mir<4>(w[i]) & ln.lom[2];
+        if constexpr (LG >= 1) w[i] ^= mir<2>(w[i]) & ln.lom[1];
+    }
+#pragma unroll
+    for (int i = 0; i < WPL; ++i) mine[i] = w[i];
+}
+
+// Information bits of the wave's CW codewords (info_pos ascending, polar_sc.py:127) from its
+// LDS u words to coalesced output rows.  info_loc[m] = (lane-in-group << 8) | slot.
 template <class C, int OUT>
-__device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs, void* __restrict__ out,
-                                       const int32_t* __restrict__ info_loc, int k, float lmax,
-                                       uint32_t* __restrict__ ulds) {
-    constexpr int N = C::N, G = C::G, LG = C::LOG_G, NS = C::NS, CW = 64 / G;
-    constexpr int WPL = (NS + 31) / 32;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int q = lane & (G - 1);
-    const int64_t cw0 = ((int64_t)blockIdx.x * kWaves + wave) * CW;
-    const int64_t cw = cw0 + (lane >> LG);
-    const float* ch = llr + (size_t)(cw < bs ? cw : bs - 1) * N;
-
-    Lane ln;
-    int res;
-    lane_layout<LG>(q, res, ln.lom);
-    ln.lom[0] = 0u;
-    ln.lmax = lmax;
-
-#if PL_SC_STAMPS
-    // diagnostic build: per-wave clock stamps into the output's tail (tools/static_probe.py)
-    uint64_t st0 = __builtin_amdgcn_s_memtime();
-#endif
-    uint64_t lo = 0, hi = 0;
-#if PL_SC_ROOT_MODE == 0
-    float chv[NS];
-#pragma unroll
-    for (int j = 0; j < NS; ++j) chv[j] = ch[j * G + res];
-#if PL_SC_STAMPS
-    __builtin_amdgcn_s_waitcnt(0);
-    for (int j = 0; j < NS; ++j) asm volatile("" : "+v"(chv[j]));
-    uint64_t st1 = __builtin_amdgcn_s_memtime();
-#endif
-    {
-        using BH = Beta<NS / 2>;
-        const BH bl = half<C, 0>(chv, 0, ln);
-        const BH br = half<C, 1>(chv, (uint64_t)bl, ln);
-        if constexpr (NS / 2 >= 64) {
-            lo = (uint64_t)(bl ^ br);
-            hi = (uint64_t)br;
-        } else {
-            lo = (uint64_t)(bl ^ br) | ((uint64_t)br << (NS / 2));
-        }
-    }
-#else
-    // Stage LOG_N-1 held in VGPRs; the channel is read once per half (the second read is
-    // served by the caches) and is never live across a half's subtree.
-#if PL_SC_STAMPS
-    uint64_t st1 = st0;
-#endif
-    {
-        using BH = Beta<NS / 2>;
-        constexpr int E = NS / 2;
-        BH bl = 0, br = 0;
-        if constexpr (nt<C>(C::LOG_N - 1, 0) != R0) {
-            float a[E];
-#pragma unroll
-            for (int j = 0; j < E; ++j) a[j] = fop<C::FM>(-ch[j * G + res], -ch[(j + E) * G + res], lmax);
-            if constexpr (E == 1) bl = lnode<C, C::LOG_N - 1, 0>(a[0], ln);
-            else bl = node<C, C::LOG_N - 1, 0>(a, ln);
-        }
-        {
-            const float* chp = ch;
-            asm volatile("" : "+v"(chp) : "v"(bl));
-            float a[E];
-#pragma unroll
-            for (int j = 0; j < E; ++j)
-                a[j] = gop(-chp[j * G + res], -chp[(j + E) * G + res], (uint32_t)(bl >> j) << 31);
-            if constexpr (E == 1) br = lnode<C, C::LOG_N - 1, N / 2>(a[0], ln);
-            else br = node<C, C::LOG_N - 1, N / 2>(a, ln);
-        }
-        if constexpr (NS / 2 >= 64) {
-            lo = (uint64_t)(bl ^ br);
-            hi = (uint64_t)br;
-        } else {
-            lo = (uint64_t)(bl ^ br) | ((uint64_t)br << (NS / 2));
-        }
-    }
-#endif
-    // u = x * G_n (G_n is an involution): in-lane spans on the packed slots, then the
-    // cross-lane spans with the mirror DPP (the low element of each pair takes the XOR).
-    {
-        constexpr uint64_t M[6] = {0x5555555555555555ull, 0x3333333333333333ull, 0x0f0f0f0f0f0f0f0full,
-                                   0x00ff00ff00ff00ffull, 0x0000ffff0000ffffull, 0x00000000ffffffffull};
-#pragma unroll
-        for (int t = 0; t < 6; ++t) {
-            if ((1 << t) < NS) {
-                lo ^= (lo >> (1 << t)) & M[t];
-                hi ^= (hi >> (1 << t)) & M[t];
-            }
-        }
-        if constexpr (NS > 64) lo ^= hi;
-        uint32_t w[4] = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
-#pragma unroll
-        for (int i = 0; i < WPL; ++i) {
-            if constexpr (LG >= 4) w[i] ^= mir<16>(w[i]) & ln.lom[4];
-            if constexpr (LG >= 3) w[i] ^= mir<8>(w[i]) & ln.lom[3];
-            if constexpr (LG >= 2) w[i] ^= mir<4>(w[i]) & ln.lom[2];
-            if constexpr (LG >= 1) w[i] ^= mir<2>(w[i]) & ln.lom[1];
-        }
-        uint32_t* mine = ulds + (wave * 64 + lane) * WPL;
-#pragma unroll
-        for (int i = 0; i < WPL; ++i) mine[i] = w[i];
-    }
-#if PL_SC_STAMPS
-    uint64_t st2 = __builtin_amdgcn_s_memtime();
-#endif
-    __syncthreads();
-#if PL_SC_STAMPS
-    uint64_t st3 = __builtin_amdgcn_s_memtime();
-#endif
-    // Information bits (info_pos ascending, polar_sc.py:127) -> coalesced rows.
-    // info_loc[m] = (lane-in-group << 8) | slot of the m-th information position.
-    const uint32_t* ubase = ulds + wave * 64 * WPL;
+__device__ __forceinline__ void emit(const uint32_t* __restrict__ ubase, int64_t cw0, int64_t bs, void* __restrict__ out,
+                                     const int32_t* __restrict__ info_loc, int k, int lane) {
+    constexpr int G = C::G, CW = 64 / G, WPL = (C::NS + 31) / 32;
     if (OUT == OUT_F32 && (k & 3) == 0 && ((reinterpret_cast<uintptr_t>(out) & 15) == 0)) {
         // 16-byte stores: lane writes info bits 4c..4c+3 of a row (1 KiB per wave-instruction)
         const int kq = k >> 2;
@@ -514,14 +526,166 @@ __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs
             }
         }
     }
+}
+
+// LDS hand-off between the lanes of ONE wave (each wave owns its LDS slots): LDS executes a
+// wave's accesses in order, so only the compiler has to be kept from reordering them.
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+template <class C>
+__device__ __forceinline__ void load_channel(float (&chv)[C::NS], const float* __restrict__ llr, int64_t cw0,
+                                             int64_t bs, int lane, int res) {
+    const int64_t cw = cw0 + (lane >> C::LOG_G);
+    const float* ch = llr + (size_t)(cw < bs ? cw : bs - 1) * C::N;
+#pragma unroll
+    for (int j = 0; j < C::NS; ++j) chv[j] = ch[j * C::G + res];
+}
+
+// Hook for half<1>: reload the channel registers with the next batch once they are dead.
+template <class C>
+struct Refill {
+    float (&chv)[C::NS];
+    const float* __restrict__ llr;
+    int64_t ncw0, bs;
+    int lane, res;
+    __device__ __forceinline__ void operator()() const {
+        // keep the scheduler from hoisting the refill above the last reads of the old values;
+        // unconditional (past the end every lane re-reads row bs-1, a cache hit) so the old
+        // values are dead here on every path
+        __builtin_amdgcn_sched_barrier(0);
+        load_channel<C>(chv, llr, ncw0, bs, lane, res);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+};
+
+template <class C, class Hook>
+__device__ __forceinline__ void root_virtual(float (&chv)[C::NS], const Lane& ln, uint64_t& lo, uint64_t& hi,
+                                             const Hook& after) {
+    constexpr int NS = C::NS;
+    using BH = Beta<NS / 2>;
+    const BH bl = half<C, 0>(chv, 0, ln);
+    const BH br = half<C, 1>(chv, (uint64_t)bl, ln, after);
+    if constexpr (NS / 2 >= 64) {
+        lo = (uint64_t)(bl ^ br);
+        hi = (uint64_t)br;
+    } else {
+        lo = (uint64_t)(bl ^ br) | ((uint64_t)br << (NS / 2));
+        hi = 0;
+    }
+}
+
+template <class C, int OUT>
+__device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs, void* __restrict__ out,
+                                       const int32_t* __restrict__ info_loc, int k, float lmax,
+                                       uint32_t* __restrict__ ulds) {
+    constexpr int N = C::N, G = C::G, LG = C::LOG_G, NS = C::NS, CW = 64 / G;
+    constexpr int WPL = (NS + 31) / 32;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int q = lane & (G - 1);
+    Lane ln;
+    int res;
+    lane_layout<LG>(q, res, ln.lom);
+    ln.lom[0] = 0u;
+    ln.lmax = lmax;
+    uint32_t* ubase = ulds + wave * 64 * WPL;
+    uint32_t* mine = ulds + (wave * 64 + lane) * WPL;
+
+#if PL_SC_PERSIST
+    // Persistent, software-pipelined: each wave walks batches of CW codewords with a stride of
+    // the whole grid; the next batch's channel is loaded into the channel registers as soon as
+    // their last read is done (3/4 through the tree), so its HBM latency overlaps the rest of
+    // the tree and the output of this batch instead of stalling every wave at the same instant.
+    const int64_t stride = (int64_t)gridDim.x * kWaves * CW;
+    int64_t cw0 = ((int64_t)blockIdx.x * kWaves + wave) * CW;
+    float chv[NS];
+    load_channel<C>(chv, llr, cw0, bs, lane, res);
+    for (; cw0 < bs; cw0 += stride) {
+        const int64_t ncw0 = cw0 + stride;
+        uint64_t lo, hi;
+        root_virtual<C>(chv, ln, lo, hi, Refill<C>{chv, llr, ncw0, bs, lane, res});
+        to_u<C>(lo, hi, ln, mine);
+        wave_lds_fence();
+        emit<C, OUT>(ubase, cw0, bs, out, info_loc, k, lane);
+        wave_lds_fence();
+    }
+#else
+    const int64_t cw0 = ((int64_t)blockIdx.x * kWaves + wave) * CW;
+#if PL_SC_STAMPS
+    // diagnostic build: per-wave clock stamps into the output's tail (tools/static_probe.py)
+    uint64_t st0 = __builtin_amdgcn_s_memtime();
+    uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    uint64_t lo = 0, hi = 0;
+#if PL_SC_ROOT_MODE == 0
+    float chv[NS];
+    load_channel<C>(chv, llr, cw0, bs, lane, res);
+#if PL_SC_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+    for (int j = 0; j < NS; ++j) asm volatile("" : "+v"(chv[j]));
+    uint64_t st1 = __builtin_amdgcn_s_memtime();
+#endif
+    root_virtual<C>(chv, ln, lo, hi, NoHook());
+#else
+    // Stage LOG_N-1 held in VGPRs; the channel is read once per half (the second read is
+    // served by the caches) and is never live across a half's subtree.
+#if PL_SC_STAMPS
+    uint64_t st1 = st0;
+#endif
+    {
+        const int64_t cw = cw0 + (lane >> LG);
+        const float* ch = llr + (size_t)(cw < bs ? cw : bs - 1) * N;
+        using BH = Beta<NS / 2>;
+        constexpr int E = NS / 2;
+        BH bl = 0, br = 0;
+        if constexpr (nt<C>(C::LOG_N - 1, 0) != R0) {
+            float a[E];
+#pragma unroll
+            for (int j = 0; j < E; ++j) a[j] = fop<C::FM>(ch[j * G + res], ch[(j + E) * G + res], lmax);
+            if constexpr (E == 1) bl = lnode<C, C::LOG_N - 1, 0>(a[0], ln) >> 31;
+            else bl = node<C, C::LOG_N - 1, 0>(a, ln);
+        }
+        {
+            const float* chp = ch;
+            asm volatile("" : "+v"(chp) : "v"(bl));
+            float a[E];
+#pragma unroll
+            for (int j = 0; j < E; ++j)
+                a[j] = (-flip31(chp[j * G + res], bit31(bl, j))) - chp[(j + E) * G + res];
+            if constexpr (E == 1) br = lnode<C, C::LOG_N - 1, N / 2>(a[0], ln) >> 31;
+            else br = node<C, C::LOG_N - 1, N / 2>(a, ln);
+        }
+        if constexpr (NS / 2 >= 64) {
+            lo = (uint64_t)(bl ^ br);
+            hi = (uint64_t)br;
+        } else {
+            lo = (uint64_t)(bl ^ br) | ((uint64_t)br << (NS / 2));
+        }
+    }
+#endif
+    to_u<C>(lo, hi, ln, mine);
+#if PL_SC_STAMPS
+    uint64_t st2 = __builtin_amdgcn_s_memtime();
+#endif
+    wave_lds_fence();
+#if PL_SC_STAMPS
+    uint64_t st3 = __builtin_amdgcn_s_memtime();
+#endif
+    emit<C, OUT>(ubase, cw0, bs, out, info_loc, k, lane);
 #if PL_SC_STAMPS
     __builtin_amdgcn_s_waitcnt(0);
     uint64_t st4 = __builtin_amdgcn_s_memtime();
+    uint64_t rt = __builtin_amdgcn_s_memrealtime();
     if (lane == 0) {
         uint64_t* d = reinterpret_cast<uint64_t*>(static_cast<float*>(out) + bs * k) + (blockIdx.x * kWaves + wave) * 8;
         d[0] = st0; d[1] = st1; d[2] = st2; d[3] = st3; d[4] = st4;
-        d[5] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));  // HW_REG_HW_ID (placement)
+        d[5] = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));  // HW_REG_HW_ID
+        d[6] = rt0;
+        d[7] = rt;
     }
+#endif
 #endif
 }
 

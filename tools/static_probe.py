@@ -58,8 +58,10 @@ def build(k, n, name, flags):
     open(src, "w").write('#include "sc_static.h"\n' + code_src(mask) + "PL_SC_STATIC_KERNELS(PlCode)\n" + r'''
 extern "C" int st_launch(const float* llr, long bs, void* out, const int* info_loc, int k, float lmax, void* st, long pf) {
     const long per = (long)pls::kWaves * (64 / PlCode::G);
-    hipLaunchKernelGGL(pl_sc_static_f32, dim3((unsigned)((bs + per - 1) / per)), dim3(64 * pls::kWaves), 0,
-                       (hipStream_t)st, llr, (int64_t)bs, out, info_loc, k, lmax, (int64_t)pf);
+    long blocks = (bs + per - 1) / per;
+    if (pf > 0 && pf < blocks) blocks = pf;  // persistent variants: pf = grid size in blocks
+    hipLaunchKernelGGL(pl_sc_static_f32, dim3((unsigned)blocks), dim3(64 * pls::kWaves), 0,
+                       (hipStream_t)st, llr, (int64_t)bs, out, info_loc, k, lmax);
     return (int)hipGetLastError();
 }
 ''')
@@ -113,6 +115,8 @@ def run(k, n, names):
                 print(f"  stamp {nm}: mean {v.mean():.0f} p10 {np.percentile(v, 10):.0f} p50 {np.median(v):.0f} p90 {np.percentile(v, 90):.0f}")
             print(f"  span {d[:, 4].max() - t0}  start spread p50 {np.median(d[:, 0] - t0):.0f} p90 {np.percentile(d[:, 0] - t0, 90):.0f}")
             np.save(os.path.join(ROOT, "gpurun_out", f"stamps_{name}.npy"), d)
+            hw = d[:, 5]
+            print("  hw_id sample:", [hex(int(v)) for v in hw[:8]], [hex(int(v)) for v in hw[1024:1032]])
             continue
         out = torch.empty((bs, k), device=dev)
         ok = True
