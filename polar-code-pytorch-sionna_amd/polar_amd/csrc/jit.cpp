@@ -250,6 +250,18 @@ int attach_static(pl_plan* p, const uint8_t* frozen, bool allow_compile) {
         (void)hipModuleUnload(mod);
         return r;
     }
+    // persistent kernels get a grid of the resident capacity (2 blocks of 4 waves per CU)
+    hipDeviceptr_t gp = nullptr;
+    size_t gsz = 0;
+    int persistent = 0;
+    if (hipModuleGetGlobal(&gp, &gsz, mod, "pl_sc_persistent") == hipSuccess && gsz == sizeof(int))
+        (void)hipMemcpyDtoH(&persistent, gp, sizeof(int));
+    (void)hipGetLastError();
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+    p->sc_persistent = persistent;
+    p->resident_blocks = 2 * cus;
     p->sc_module = mod;
     p->sc_fn_f32 = f32;
     p->sc_fn_u8 = u8;
@@ -267,7 +279,8 @@ int launch_sc_static(const pl_plan* p, const float* llr, int64_t bs, void* out, 
     if (bs == 0 || p->k == 0) return PL_OK;
     const int G = 1 << static_log_g(p->log_n);
     const int64_t per_block = 4 * (64 / G);  // pls::kWaves codeword groups of 64/G
-    const int64_t blocks = (bs + per_block - 1) / per_block;
+    int64_t blocks = (bs + per_block - 1) / per_block;
+    if (p->sc_persistent && p->resident_blocks > 0 && blocks > p->resident_blocks) blocks = p->resident_blocks;
     if (blocks > 0x7fffffffLL) {
         set_error("SC decode: batch too large for one launch");
         return PL_EINVAL;

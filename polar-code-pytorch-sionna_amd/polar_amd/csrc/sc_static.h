@@ -693,6 +693,7 @@ __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs
 
 // Entry points instantiated per code: the including translation unit defines PlCode first.
 #define PL_SC_STATIC_KERNELS(CODE)                                                                           \
+    extern "C" __device__ const int pl_sc_persistent = PL_SC_PERSIST;                                       \
     extern "C" __global__ __launch_bounds__(64 * pls::kWaves, PL_SC_MINW) void pl_sc_static_f32(                      \
         const float* __restrict__ llr, int64_t bs, void* __restrict__ out, const int32_t* __restrict__ info_loc, \
         int k, float lmax) {                                                                                  \
