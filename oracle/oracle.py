@@ -34,7 +34,13 @@ def lib():
         L.orc_scl_decode.argtypes = [i32, P, i32, P, i64, P, P, i32]
         L.orc_scl_decode_lazy.argtypes = [i32, P, i32, P, i64, P, P, i32]
         L.orc_polar_encode.argtypes = [i32, P, P, i64, P]
-        for f in (L.orc_sc_decode, L.orc_scl_decode, L.orc_scl_decode_lazy, L.orc_polar_encode):
+        L.orc_scl_decode_mysn.argtypes = [i32, P, i32, P, i64, P, P, i32, i32, i32, ctypes.c_uint32, i32]
+        L.orc_crc_encode.argtypes = [P, i64, i32, i32, ctypes.c_uint32, P]
+        L.orc_crc_check.argtypes = [P, i64, i32, i32, ctypes.c_uint32, P]
+        L.orc_np_pairwise_sum.argtypes = [P, i32]
+        L.orc_np_pairwise_sum.restype = ctypes.c_double
+        for f in (L.orc_sc_decode, L.orc_scl_decode, L.orc_scl_decode_lazy, L.orc_polar_encode,
+                  L.orc_scl_decode_mysn, L.orc_crc_encode, L.orc_crc_check):
             f.restype = i32
         _lib = L
     return _lib
@@ -88,3 +94,58 @@ def polar_encode(u_bits, frozen_pos, n):
     out = np.empty((bs, n), dtype=np.float32)
     lib().orc_polar_encode(n, _ptr(fm), _ptr(u), bs, _ptr(out))
     return out
+
+
+# 5G CRC polynomials, 3GPP TS 38.212 Sec. 5.1 as listed in my_sn/fec/crc.py:38-52 (exponents)
+CRC_POLYS = {"CRC24A": [24, 23, 18, 17, 14, 11, 10, 7, 6, 5, 4, 3, 1, 0], "CRC24B": [24, 23, 6, 5, 1, 0],
+             "CRC24C": [24, 23, 21, 20, 17, 15, 13, 12, 8, 4, 2, 1, 0], "CRC16": [16, 12, 5, 0],
+             "CRC11": [11, 10, 9, 5, 0], "CRC6": [6, 5, 0]}
+
+
+def crc_params(name):
+    """(degree, generator mask without the leading term) of a 5G CRC polynomial."""
+    ex = CRC_POLYS[name]
+    deg = ex[0]
+    return deg, sum(1 << e for e in ex if e < deg)
+
+
+def crc_encode(bits, name):
+    """CRCEncoder.forward (crc.py:85-104): [bs, k] 0/1 -> [bs, k + deg] float32."""
+    x = np.ascontiguousarray(bits, dtype=np.float32)
+    bs, k = x.shape
+    deg, g = crc_params(name)
+    out = np.empty((bs, k + deg), dtype=np.float32)
+    assert lib().orc_crc_encode(_ptr(x), bs, k, deg, g, _ptr(out)) == 0
+    return out
+
+
+def crc_check(bits, name):
+    """CRCDecoder validity (crc.py:119-138): [bs, k+deg] -> bool [bs]."""
+    x = np.ascontiguousarray(bits, dtype=np.float32)
+    bs, n = x.shape
+    deg, g = crc_params(name)
+    v = np.empty(bs, dtype=np.uint8)
+    assert lib().orc_crc_check(_ptr(x), bs, n, deg, g, _ptr(v)) == 0
+    return v.astype(bool)
+
+
+def np_pairwise_sum(a):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    return lib().orc_np_pairwise_sum(_ptr(a), int(a.shape[0]))
+
+
+def scl_decode_mysn(llr_logits, frozen_pos, list_size=8, fast_scl=True, exact_f=True, crc=None, nthreads=0):
+    """my_sn SCL_Dec.forward (dec.py:158-537): exact f, fast-SCL, optional CRC-aided pick.
+    Returns (bits float32 [bs,k], msg_pm float64 [bs,2L]: sorted, then CRC-penalised in place)."""
+    x = np.ascontiguousarray(llr_logits, dtype=np.float32)
+    bs, n = x.shape
+    fm = frozen_mask(frozen_pos, n)
+    k = int(n - fm.sum())
+    out = np.empty((bs, k), dtype=np.float32)
+    pm = np.empty((bs, 2 * list_size), dtype=np.float64)
+    deg, g = crc_params(crc) if crc else (0, 0)
+    r = lib().orc_scl_decode_mysn(n, _ptr(fm), int(list_size), _ptr(x), bs, _ptr(out), _ptr(pm), int(bool(fast_scl)),
+                                  int(bool(exact_f)), deg, g, int(nthreads))
+    if r < 0:
+        raise ValueError("orc_scl_decode_mysn rejected its arguments")
+    return out, pm

@@ -21,6 +21,13 @@
  *                   against orc_scl_decode in tests.
  *   orc_polar_encode  x_run_sn_polar/polar/enc.py:30-43 (c[:,info]=u; (c@G)%2) computed by the
  *                   XOR butterfly of my_sn/fec/polar/enc.py:85-96.
+ *   orc_crc_encode / orc_crc_check  my_sn/fec/crc.py: CRCEncoder (:6-109, G-matrix form of the
+ *                   5G polynomials :38-52) and CRCDecoder (:111-138), restated as the MSB-first
+ *                   shift register (equal to the G-matrix form; pinned by tests/golden/crc.npz).
+ *   orc_scl_decode_mysn  my_sn/fec/polar/dec.py SCL_Dec (:158-537): exact-boxplus f (:330-339),
+ *                   fast-SCL rate-0 (:269-280) and repetition (:281-306) nodes with numpy's
+ *                   pairwise summation order for the node sums, CRC-aided pick (:507-518).
+ *                   Same stable tie order as orc_scl_decode.
  */
 #include <math.h>
 #include <stdint.h>
@@ -370,6 +377,244 @@ int orc_scl_decode_lazy(int n, const uint8_t* frozen_mask, int L, const float* l
         }
         free(ch); free(c.alpha); free(c.sptr); free(c.beta); free(c.u);
         free(c.tmp_beta); free(c.tmp_u); free(c.tmp_sptr);
+    }
+    free(info);
+    return k;
+}
+
+/* ------------------------------------------- my_sn SCL (fast-SCL, CRC) ---- */
+/* np.sum over the last axis of a contiguous float64 array: numpy's pairwise summation
+ * (blocks of <= 128 with 8 interleaved partial sums, halves above).  Pinned against numpy in
+ * tests/test_oracle.py. */
+double orc_np_pairwise_sum(const double* a, int n) {
+    if (n < 8) {
+        double r = 0.0;
+        for (int i = 0; i < n; ++i) r += a[i];
+        return r;
+    }
+    if (n <= 128) {
+        double r[8];
+        for (int j = 0; j < 8; ++j) r[j] = a[j];
+        int i = 8;
+        for (; i < n - (n % 8); i += 8)
+            for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; ++i) res += a[i];
+        return res;
+    }
+    int n2 = n / 2;
+    n2 -= n2 % 8;
+    return orc_np_pairwise_sum(a, n2) + orc_np_pairwise_sum(a + n2, n - n2);
+}
+
+/* CRC remainder of bits[0..len) (MSB first) times D^deg modulo g, g given by its coefficient
+ * bit mask without the leading term (bit c set = D^c present, c < deg). */
+static uint32_t crc_reg(const uint8_t* bits, int len, int deg, uint32_t g) {
+    uint32_t reg = 0, mask = (deg == 32) ? 0xffffffffu : ((1u << deg) - 1u);
+    for (int i = 0; i < len; ++i) {
+        const uint32_t fb = ((reg >> (deg - 1)) & 1u) ^ (bits[i] & 1u);
+        reg = (reg << 1) & mask;
+        if (fb) reg ^= g;
+    }
+    return reg;
+}
+
+/* CRCEncoder.forward: [bs, k] 0/1 -> [bs, k + deg] (systematic, parity appended MSB first). */
+int orc_crc_encode(const float* in, int64_t bs, int k, int deg, uint32_t g, float* out) {
+    if (deg < 1 || deg > 31 || k < 0) return -1;
+    uint8_t* b = (uint8_t*)malloc((size_t)k + 1);
+    for (int64_t r = 0; r < bs; ++r) {
+        for (int i = 0; i < k; ++i) b[i] = in[r * k + i] != 0.0f;
+        const uint32_t reg = crc_reg(b, k, deg, g);
+        for (int i = 0; i < k; ++i) out[r * (k + deg) + i] = (float)b[i];
+        for (int i = 0; i < deg; ++i) out[r * (k + deg) + k + i] = (float)((reg >> (deg - 1 - i)) & 1u);
+    }
+    free(b);
+    return 0;
+}
+
+/* CRCDecoder.forward validity: re-encoding the whole (info||parity) word gives zero parity. */
+int orc_crc_check(const float* in, int64_t bs, int len, int deg, uint32_t g, uint8_t* valid) {
+    if (deg < 1 || deg > 31 || len < deg) return -1;
+    uint8_t* b = (uint8_t*)malloc((size_t)len + 1);
+    for (int64_t r = 0; r < bs; ++r) {
+        for (int i = 0; i < len; ++i) b[i] = in[r * len + i] != 0.0f;
+        valid[r] = crc_reg(b, len, deg, g) == 0u;
+    }
+    free(b);
+    return 0;
+}
+
+static inline double f_exact_d(double x, double y) {  /* dec.py:330-339 on float64 */
+    const double xc = fmax(fmin(x, 30.0), -30.0), yc = fmax(fmin(y, 30.0), -30.0);
+    double o = log(1.0 + exp(xc + yc));
+    o -= log(exp(xc) + exp(yc));
+    return o;
+}
+
+typedef struct {
+    lz_ctx z;
+    int fast, exact;
+    double* terms;  /* [n] scratch for node sums */
+} my_ctx;
+
+/* stable selection of L survivors among 2L candidates + fork (dec.py:315-330, :340-352) */
+static void my_select(lz_ctx* c, const double* cand, int a, int len) {
+    const int L = c->L, n = c->n, S1 = c->S + 1;
+    int src[32], bit[32];
+    double npm[32];
+    for (int i = 0; i < 2 * L; ++i) {
+        int r = 0;
+        for (int j = 0; j < 2 * L; ++j) r += (cand[j] < cand[i]) || (cand[j] == cand[i] && j < i);
+        if (r < L) { src[r] = i % L; bit[r] = i / L; npm[r] = cand[i]; }
+    }
+    memcpy(c->tmp_beta, c->beta, (size_t)L * n);
+    memcpy(c->tmp_u, c->u, (size_t)L * n);
+    memcpy(c->tmp_sptr, c->sptr, sizeof(int) * (size_t)L * S1);
+    for (int m = 0; m < L; ++m) {
+        const int q = src[m];
+        memcpy(c->beta + (size_t)m * n, c->tmp_beta + (size_t)q * n, (size_t)n);
+        memcpy(c->u + (size_t)m * n, c->tmp_u + (size_t)q * n, (size_t)n);
+        memcpy(c->sptr + (size_t)m * S1, c->tmp_sptr + (size_t)q * S1, sizeof(int) * S1);
+        for (int j = a; j < a + len; ++j) c->beta[(size_t)m * n + j] = (uint8_t)bit[m];  /* node partial sums */
+        c->u[(size_t)m * n + a + len - 1] = (uint8_t)bit[m];                              /* its info bit */
+        c->pm[m] = npm[m];
+    }
+}
+
+static void my_node(my_ctx* mc, int a, int s) {
+    lz_ctx* c = &mc->z;
+    const int n = c->n, L = c->L, S1 = c->S + 1, len = 1 << s;
+    if (s > 0 && mc->fast) {
+        int nfz = 0;
+        for (int j = a; j < a + len; ++j) nfz += c->frozen[j] != 0;
+        if (nfz == len) {  /* rate-0 (dec.py:269-280): pm += sum softplus(-clip(llr)) */
+            for (int p = 0; p < L; ++p) {
+                const double* in = lz_stage(c, p, s);
+                for (int j = 0; j < len; ++j) mc->terms[j] = log(1.0 + exp(-fmax(fmin(in[j], 30.0), -30.0)));
+                c->pm[p] += orc_np_pairwise_sum(mc->terms, len);
+                memset(c->beta + (size_t)p * n + a, 0, (size_t)len);
+            }
+            return;
+        }
+        if (!c->frozen[a + len - 1] && nfz == len - 1) {  /* repetition (dec.py:281-306) */
+            double cand[64];
+            for (int p = 0; p < L; ++p) {
+                const double* in = lz_stage(c, p, s);
+                for (int j = 0; j < len; ++j) mc->terms[j] = log(1.0 + exp(-fmax(fmin(in[j], 30.0), -30.0)));
+                cand[p] = c->pm[p] + orc_np_pairwise_sum(mc->terms, len);
+                for (int j = 0; j < len; ++j) mc->terms[j] = log(1.0 + exp(-fmax(fmin(-in[j], 30.0), -30.0)));
+                cand[L + p] = c->pm[p] + orc_np_pairwise_sum(mc->terms, len);
+            }
+            my_select(c, cand, a, len);
+            return;
+        }
+    }
+    if (s > 0) {
+        const int h = 1 << (s - 1);
+        for (int p = 0; p < L; ++p) {
+            const double* in = lz_stage(c, p, s);
+            double* out = c->alpha + (size_t)p * n + (1u << (s - 1));
+            for (int j = 0; j < h; ++j) out[j] = mc->exact ? f_exact_d(in[j], in[j + h]) : f_minsum_d(in[j], in[j + h]);
+        }
+        for (int p = 0; p < L; ++p) c->sptr[p * S1 + s - 1] = p;
+        my_node(mc, a, s - 1);
+        for (int p = 0; p < L; ++p) {
+            const double* in = lz_stage(c, p, s);
+            double* out = c->alpha + (size_t)p * n + (1u << (s - 1));
+            const uint8_t* bl = c->beta + (size_t)p * n + a;
+            for (int j = 0; j < h; ++j) out[j] = (bl[j] ? -in[j] : in[j]) + in[j + h];
+        }
+        for (int p = 0; p < L; ++p) c->sptr[p * S1 + s - 1] = p;
+        my_node(mc, a + h, s - 1);
+        for (int p = 0; p < L; ++p) {
+            uint8_t* b = c->beta + (size_t)p * n + a;
+            for (int j = 0; j < h; ++j) b[j] ^= b[j + h];
+        }
+        return;
+    }
+    /* leaf (dec.py:377-383): pm update every leaf; info leaves select and fork */
+    double cand[64];
+    for (int p = 0; p < L; ++p) {
+        const double l = fmax(fmin(lz_stage(c, p, 0)[0], 30.0), -30.0);
+        cand[p] = c->pm[p] + log(1.0 + exp(-l));
+        cand[L + p] = c->pm[p] + log(1.0 + exp(-(-1.0 * l)));
+    }
+    if (c->frozen[a]) {
+        for (int p = 0; p < L; ++p) { c->pm[p] = cand[p]; c->beta[(size_t)p * n + a] = 0; c->u[(size_t)p * n + a] = 0; }
+        return;
+    }
+    my_select(c, cand, a, 1);
+}
+
+/* SCL_Dec.forward of my_sn (dec.py:476-537).  crc_deg = 0: no CRC.  out_pm = msg_pm as the
+ * reference leaves it: sorted by _decode_np_batch, then CRC-penalised in place, [bs][2L]. */
+int orc_scl_decode_mysn(int n, const uint8_t* frozen_mask, int L, const float* logits, int64_t bs, float* out_bits,
+                        double* out_pm, int fast_scl, int exact_f, int crc_deg, uint32_t crc_g, int nthreads) {
+    const int S = ilog2(n);
+    if (S < 0 || L < 1 || L > 32 || (L & (L - 1)) || !frozen_mask || !logits || !out_bits) return -1;
+    int* info = (int*)malloc(sizeof(int) * (size_t)n);
+    int k = 0;
+    for (int i = 0; i < n; ++i) if (!frozen_mask[i]) info[k++] = i;
+    if (crc_deg > 0 && k < crc_deg) { free(info); return -1; }
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel
+#endif
+    {
+        my_ctx mc;
+        lz_ctx* c = &mc.z;
+        mc.fast = fast_scl; mc.exact = exact_f;
+        c->n = n; c->S = S; c->L = L; c->frozen = frozen_mask;
+        double* ch = (double*)malloc(sizeof(double) * (size_t)n);
+        c->ch = ch;
+        c->alpha = (double*)malloc(sizeof(double) * (size_t)L * n);
+        c->sptr = (int*)malloc(sizeof(int) * (size_t)L * (S + 1));
+        c->beta = (uint8_t*)malloc((size_t)L * n);
+        c->u = (uint8_t*)malloc((size_t)L * n);
+        c->tmp_beta = (uint8_t*)malloc((size_t)L * n);
+        c->tmp_u = (uint8_t*)malloc((size_t)L * n);
+        c->tmp_sptr = (int*)malloc(sizeof(int) * (size_t)L * (S + 1));
+        mc.terms = (double*)malloc(sizeof(double) * (size_t)n);
+        uint8_t* ub = (uint8_t*)malloc((size_t)k + 1);
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 4)
+#endif
+        for (int64_t b = 0; b < bs; ++b) {
+            for (int i = 0; i < n; ++i) ch[i] = (double)(-1.0f * logits[b * n + i]);
+            memset(c->beta, 0, (size_t)L * n);
+            memset(c->u, 0, (size_t)L * n);
+            for (int p = 0; p < L * (S + 1); ++p) c->sptr[p] = p / (S + 1);
+            for (int p = 0; p < L; ++p) c->pm[p] = p == 0 ? 0.0 : 30.0;
+            my_node(&mc, 0, S);
+            /* final sort (dec.py:202) of the 2L logical rows (row r < L = state r, row r >= L its
+             * copy), stable by pm; CRC penalty 30*k per failing row added in place (dec.py:515-518,
+             * which also lands in the returned msg_pm: it aliases self.msg_pm); first argmin. */
+            int row[64];
+            for (int r = 0; r < 2 * L; ++r) row[r] = r;
+            for (int i = 1; i < 2 * L; ++i) {
+                int v = row[i], j = i - 1;
+                while (j >= 0 && c->pm[row[j] % L] > c->pm[v % L]) { row[j + 1] = row[j]; --j; }
+                row[j + 1] = v;
+            }
+            int fail[32] = {0};
+            if (crc_deg > 0)
+                for (int p = 0; p < L; ++p) {
+                    for (int m = 0; m < k; ++m) ub[m] = c->u[(size_t)p * n + info[m]];
+                    fail[p] = crc_reg(ub, k, crc_deg, crc_g) != 0u;
+                }
+            int best = row[0] % L;
+            double bestv = 0.0;
+            for (int r = 0; r < 2 * L; ++r) {
+                const int p = row[r] % L;
+                const double v = c->pm[p] + (fail[p] ? 30.0 * (double)k : 0.0);
+                if (out_pm) out_pm[b * 2 * L + r] = v;
+                if (r == 0 || v < bestv) { best = p; bestv = v; }
+            }
+            for (int m = 0; m < k; ++m) out_bits[b * k + m] = (float)c->u[(size_t)best * n + info[m]];
+        }
+        free(ch); free(c->alpha); free(c->sptr); free(c->beta); free(c->u);
+        free(c->tmp_beta); free(c->tmp_u); free(c->tmp_sptr); free(mc.terms); free(ub);
     }
     free(info);
     return k;

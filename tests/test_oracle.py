@@ -96,3 +96,39 @@ def test_oracle_roundtrip_noiseless():
     x = oracle.polar_encode(u, fp, 1024)
     logits = (2 * x - 1) * 4.0  # logits > 0 mean bit 1
     assert np.array_equal(oracle.sc_decode(logits, fp), u)
+
+
+# ---- my_sn extras: CRC, numpy pairwise sums, my_sn SCL_Dec ---------------
+def test_oracle_numpy_pairwise_sum_matches_numpy():
+    rng = np.random.default_rng(3)
+    for n in (1, 2, 3, 7, 8, 9, 16, 100, 128, 129, 256, 512, 1000, 1024):
+        for _ in range(20):
+            a = rng.standard_normal(n) * np.exp(rng.standard_normal(n) * 3)
+            assert oracle.np_pairwise_sum(a) == np.sum(a[None, None, :], axis=-1)[0, 0]
+
+
+def test_oracle_crc_matches_reference_fixture(golden_dir):
+    d = np.load(os.path.join(golden_dir, "crc.npz"))
+    n = 0
+    for key in d.files:
+        if not key.endswith("_u"):
+            continue
+        base = key[:-2]
+        name = base.split("_k")[0]
+        assert np.array_equal(oracle.crc_encode(d[key], name), d[base + "_enc"]), base
+        assert np.array_equal(oracle.crc_check(d[base + "_word"], name), d[base + "_valid"].astype(bool)), base
+        n += 1
+    assert n == 18
+
+
+@pytest.mark.parametrize("fname,kw", [("mysn_scl_L8_32_64", {}), ("mysn_scl_L8_128_256", {}),
+                                      ("mysn_scl_nofast_L4_32_64", {"fast_scl": False}),
+                                      ("mysn_scl_crc11_L8_32_64", {"crc": "CRC11"}),
+                                      ("mysn_scl_crc24c_L8_128_256", {"crc": "CRC24C"})])
+def test_oracle_mysn_scl_matches_reference(golden_dir, fname, kw):
+    d = np.load(os.path.join(golden_dir, fname + ".npz"))
+    for name in [k[4:] for k in d.files if k.startswith("llr_")]:
+        b, pm = oracle.scl_decode_mysn(d["llr_" + name], d["frozen_pos"], int(d["L"]), **kw)
+        assert np.array_equal(b.astype(np.uint8), d["bits_stable_" + name]), name
+        assert np.array_equal(b.astype(np.uint8), d["bits_" + name]), name
+        assert np.abs(pm - d["pm_stable_" + name]).max() < 1e-9, name
