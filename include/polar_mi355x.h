@@ -42,6 +42,9 @@ extern "C" {
 
 #define PL_PLAN_GENERIC 1u    /* pl_plan_create flag: never specialise the SC kernel */
 #define PL_PLAN_CACHE_ONLY 2u /* pl_plan_create flag: use a cached specialised kernel, never compile */
+#define PL_PLAN_FAST_SCL 4u   /* pl_plan_create flag (SCL): fast-SCL rate-0 / repetition pruning of
+                                 my_sn/fec/polar/dec.py:367-376 (use with f_mode PL_F_EXACT for
+                                 my_sn SCL_Dec semantics) */
 
 #define PL_KERNEL_GENERIC 0     /* pl_plan_kernel kinds */
 #define PL_KERNEL_SPECIALIZED 1
@@ -83,6 +86,12 @@ int pl_scl_decode(const pl_plan* plan, const float* llr_logits, int64_t bs, void
 /* Polar encoding with the plan's frozen set: u_bits [bs, k] fp32 0/1 -> codewords [bs, n] fp32. */
 int pl_polar_encode(const pl_plan* plan, const float* u_bits, int64_t bs, float* codewords,
                     void* hip_stream);
+
+/* CRC-aided SCL (my_sn/fec/polar/dec.py:507-518): after decoding, every path whose k decoded
+ * bits fail the CRC (generator x^degree + sum of the bits of poly_mask, MSB-first shift register,
+ * my_sn/fec/crc.py) gets +30*k on its metric before the first argmin.  degree 0 turns it off.
+ * Call before the plan's first decode.  Replaces SCL_Dec(crc_degree=...) (dec.py:210-218). */
+int pl_plan_set_crc(pl_plan* plan, int32_t degree, uint32_t poly_mask);
 
 /* Which SC kernel a plan launches: *kind = PL_KERNEL_GENERIC / PL_KERNEL_SPECIALIZED; path
  * (nullable) receives the code object file of a specialised kernel. */

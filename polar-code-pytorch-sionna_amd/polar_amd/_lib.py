@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(_HERE, "libpolar_mi355x.so")
 PL_OK, PL_EINVAL, PL_EHIP, PL_ENOTSUP = 0, -1, -2, -3
 PL_F_MINSUM, PL_F_EXACT = 0, 1
 PL_OUT_F32, PL_OUT_U8 = 0, 1
-PL_PLAN_GENERIC, PL_PLAN_CACHE_ONLY = 1, 2
+PL_PLAN_GENERIC, PL_PLAN_CACHE_ONLY, PL_PLAN_FAST_SCL = 1, 2, 4
 PL_KERNEL_GENERIC, PL_KERNEL_SPECIALIZED = 0, 1
 
 _lock = threading.Lock()
@@ -39,11 +39,12 @@ def _declare(L):
     L.pl_scl_decode.argtypes = [P, P, i64, P, i32, P, P, ctypes.c_size_t, P]
     L.pl_polar_encode.argtypes = [P, P, i64, P, P]
     L.pl_plan_kernel.argtypes = [P, P, ctypes.c_char_p, ctypes.c_size_t]
+    L.pl_plan_set_crc.argtypes = [P, i32, u32]
     L.pl_sc_specialize.argtypes = [i32, P, i32, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
     L.pl_last_error_string.restype = ctypes.c_char_p
     L.pl_version.restype = ctypes.c_char_p
     for f in (L.pl_plan_create, L.pl_plan_destroy, L.pl_plan_info, L.pl_sc_decode, L.pl_scl_decode,
-              L.pl_polar_encode, L.pl_plan_kernel, L.pl_sc_specialize):
+              L.pl_polar_encode, L.pl_plan_kernel, L.pl_sc_specialize, L.pl_plan_set_crc):
         f.restype = ctypes.c_int
     return L
 
@@ -64,7 +65,8 @@ def lib():
 
 EXPORTED_SYMBOLS = ("pl_plan_create", "pl_plan_destroy", "pl_plan_info", "pl_sc_decode",
                     "pl_scl_workspace_size", "pl_scl_decode", "pl_polar_encode",
-                    "pl_plan_kernel", "pl_sc_specialize", "pl_last_error_string", "pl_version")
+                    "pl_plan_kernel", "pl_sc_specialize", "pl_plan_set_crc", "pl_last_error_string",
+                    "pl_version")
 
 
 def check(rc, what):
@@ -98,6 +100,10 @@ class Plan:
     @property
     def handle(self):
         return self._h
+
+    def set_crc(self, degree, poly_mask):
+        """CRC-aided path selection for SCL plans (pl_plan_set_crc)."""
+        check(lib().pl_plan_set_crc(self._h, int(degree), int(poly_mask)), "pl_plan_set_crc")
 
     def kernel(self):
         """('specialized' | 'generic', code-object path or '') of the SC kernel this plan runs."""

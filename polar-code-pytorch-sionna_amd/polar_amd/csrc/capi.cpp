@@ -168,6 +168,17 @@ int pl_plan_destroy(pl_plan* plan) {
     return PL_OK;
 }
 
+int pl_plan_set_crc(pl_plan* p, int32_t degree, uint32_t poly_mask) {
+    if (!p || degree < 0 || degree > 31 || (degree > 0 && p->k < degree) ||
+        (degree > 0 && (poly_mask >> degree) != 0u)) {
+        pl::set_error("pl_plan_set_crc: bad arguments (0 <= degree <= min(31, k), mask below x^degree)");
+        return PL_EINVAL;
+    }
+    p->crc_deg = degree;
+    p->crc_g = degree > 0 ? poly_mask : 0u;
+    return PL_OK;
+}
+
 int pl_plan_info(const pl_plan* p, int32_t* n, int32_t* k, int32_t* list_size) {
     if (!p) {
         pl::set_error("pl_plan_info: null plan");

@@ -21,6 +21,8 @@ struct pl_plan {
     hipModule_t sc_module = nullptr;
     hipFunction_t sc_fn_f32 = nullptr, sc_fn_u8 = nullptr;
     std::string kernel_path;             // code object the module came from
+    int32_t crc_deg = 0;                 // SCL CRC-aided pick: degree (0 = none) and generator
+    uint32_t crc_g = 0;                  //   mask without the leading term
     int32_t sc_persistent = 0;           // kernel walks batches with a grid stride (grid capped)
     int32_t resident_blocks = 0;         // 256-thread blocks resident at 2 waves/SIMD on the device
 };

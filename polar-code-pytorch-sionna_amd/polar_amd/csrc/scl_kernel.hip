@@ -20,6 +20,15 @@
 // each fork, n/32 words each), the fp32 channel (stage S).  Stage S-1 is never stored: it is
 // recomputed from the channel (f for the left half, g with the path's own partial sums for the
 // right half), which halves the footprint (about 38 KB per codeword at n=1024, L=8).
+//
+// my_sn variant (my_sn/fec/polar/dec.py SCL_Dec :158-537), selected per plan:
+//   FM = 1    exact boxplus f on clipped inputs, float64 (dec.py:330-339)
+//   FAST      fast-SCL tree pruning (dec.py:367-376): a rate-0 node adds, per path, the sum of
+//             log(1+exp(-clip(llr))) over the node (:269-280); a repetition node forks once on
+//             the two node sums (:281-306).  Sums follow numpy's pairwise order (np.sum over the
+//             last axis) so path metrics match to rounding.
+//   CRC       CRC-aided pick (:507-518): every path failing the CRC gets +30*k, first argmin; the
+//             penalty also lands in the returned metrics (it aliases msg_pm in the reference).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -74,17 +83,29 @@ __device__ __forceinline__ double f_ms(double x, double y, double lmax) {  // po
     const bool neg = (__double_as_longlong(x) ^ __double_as_longlong(y)) < 0;
     return neg ? -m : m;
 }
+__device__ __forceinline__ double f_ex(double x, double y, double lmax) {  // my_sn dec.py:330-339
+    const double xc = fmax(fmin(x, lmax), -lmax), yc = fmax(fmin(y, lmax), -lmax);
+    double o = log(1.0 + exp(xc + yc));
+    o -= log(exp(xc) + exp(yc));
+    return o;
+}
+template <int FM>
+__device__ __forceinline__ double f_op(double x, double y, double lmax) {
+    if constexpr (FM == 0) return f_ms(x, y, lmax);
+    else return f_ex(x, y, lmax);
+}
 __device__ __forceinline__ double g_op(double x, double y, uint32_t bit) {  // :107-108
     return (bit ? -x : x) + y;
 }
 __device__ __forceinline__ uint32_t getbit(const uint32_t* w, int pos) { return (w[pos >> 5] >> (pos & 31)) & 1u; }
 
 // LLR j of the stage-s node at position pos for path p.
+template <int FM>
 __device__ __forceinline__ double read_alpha(const St& t, int p, int s, int pos, int j) {
     if (s == t.S) return (double)t.ch[j];
     if (s == t.S - 1) {
         const double x = (double)t.ch[j], y = (double)t.ch[j + t.half];
-        if (pos == 0) return f_ms(x, y, t.lmax);
+        if (pos == 0) return f_op<FM>(x, y, t.lmax);
         return g_op(x, y, getbit(t.beta + p * t.W, j));
     }
     const int owner = t.sptr[p * t.S + s];
@@ -92,14 +113,15 @@ __device__ __forceinline__ double read_alpha(const St& t, int p, int s, int pos,
 }
 
 // f (is_g = false) or g at the stage-s node at position pos, for every path: writes stage s-1.
+template <int FM>
 __device__ void node_fg(St& t, int s, int pos, bool is_g, int lane) {
     const int ls = s - 1, h = 1 << ls;
     const int total = t.L * h;
     for (int idx = lane; idx < total; idx += 64) {
         const int p = idx >> ls, j = idx & (h - 1);
-        const double x = read_alpha(t, p, s, pos, j);
-        const double y = read_alpha(t, p, s, pos, j + h);
-        const double r = is_g ? g_op(x, y, getbit(t.beta + p * t.W, pos + j)) : f_ms(x, y, t.lmax);
+        const double x = read_alpha<FM>(t, p, s, pos, j);
+        const double y = read_alpha<FM>(t, p, s, pos, j + h);
+        const double r = is_g ? g_op(x, y, getbit(t.beta + p * t.W, pos + j)) : f_op<FM>(x, y, t.lmax);
         t.A[p * t.half + h + j] = r;
     }
     __syncthreads();
@@ -133,22 +155,11 @@ __device__ __forceinline__ double shfl_d(double v, int src) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
-// Leaf i: path-metric update for every path; at information leaves the 2L-candidate selection
-// and the fork (inherit parent's pointers, partial sums and decisions, then set bit i).
-__device__ void leaf(St& t, int i, bool info, int lane) {
-    double pen0 = 0.0, pen1 = 0.0, pmv = 0.0;
-    if (lane < t.L) {
-        double l = read_alpha(t, lane, 0, i, 0);
-        l = fmax(fmin(l, t.lmax), -t.lmax);
-        pmv = t.pm[lane];
-        pen0 = log(1.0 + exp(-(1.0 * l)));
-        pen1 = info ? log(1.0 + exp(-(-1.0 * l))) : 0.0;
-    }
-    if (!info) {
-        if (lane < t.L) t.pm[lane] = pmv + pen0;
-        __syncthreads();
-        return;
-    }
+// 2L-candidate selection and fork (polar_scl.py:86-92 + :109-120): lanes < L hold pm + pen0
+// (candidate c = state c, u = 0) and pen1 (candidate L + c = state c, u = 1).  Survivors take
+// their parent's partial sums, decisions and stage pointers; a fork on a node [a, a+len) sets
+// the node's partial sums to the chosen bit (len = 1: a leaf) and its last decision.
+__device__ void select_fork(St& t, double pmv, double pen0, double pen1, int a, int len, int lane) {
     const int L = t.L;
     // candidate c: c < L -> (state c, u=0), c >= L -> (state c-L, u=1)
     const int src = lane < L ? lane : (lane - L);
@@ -190,15 +201,19 @@ __device__ void leaf(St& t, int i, bool info, int lane) {
         if (idx < L * S) sp[r] = t.sptr[t.fpar[idx / S] * S + idx % S];
     }
     __syncthreads();
+    const int last = a + len - 1;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int idx = r * 64 + lane;
         if (idx < per) {
             const int np = idx / W, w = idx - np * W;
             uint32_t b = vb[r], uu = vu[r];
-            if (w == (i >> 5) && t.fbit[np]) {
-                b |= 1u << (i & 31);
-                uu |= 1u << (i & 31);
+            if (t.fbit[np]) {
+                // node bits [a, a+len) inside word w
+                const int lo = a > (w << 5) ? a - (w << 5) : 0;
+                const int hi = (a + len) < ((w + 1) << 5) ? (a + len) - (w << 5) : 32;
+                if (lo < hi) b |= (hi - lo == 32 ? 0xffffffffu : (((1u << (hi - lo)) - 1u) << lo));
+                if (w == (last >> 5)) uu |= 1u << (last & 31);
             }
             t.beta[np * W + w] = b;
             t.u[np * W + w] = uu;
@@ -213,12 +228,101 @@ __device__ void leaf(St& t, int i, bool info, int lane) {
     __syncthreads();
 }
 
-template <int OUTK>
+// Leaf i: path-metric update for every path (polar_scl.py:69-85); at information leaves the
+// 2L-candidate selection and fork.
+template <int FM>
+__device__ void leaf(St& t, int i, bool info, int lane) {
+    double pen0 = 0.0, pen1 = 0.0, pmv = 0.0;
+    if (lane < t.L) {
+        double l = read_alpha<FM>(t, lane, 0, i, 0);
+        l = fmax(fmin(l, t.lmax), -t.lmax);
+        pmv = t.pm[lane];
+        pen0 = log(1.0 + exp(-(1.0 * l)));
+        pen1 = info ? log(1.0 + exp(-(-1.0 * l))) : 0.0;
+    }
+    if (!info) {
+        if (lane < t.L) t.pm[lane] = pmv + pen0;
+        __syncthreads();
+        return;
+    }
+    select_fork(t, pmv, pen0, pen1, i, 1, lane);
+}
+
+// Sum of log(1+exp(-clip(sg*llr))) over the stage-s node at pos for path p, in numpy's pairwise
+// order (np.sum over the last axis: < 8 terms sequentially from 0; <= 128 terms with 8
+// interleaved partial sums combined ((0+1)+(2+3))+((4+5)+(6+7)); larger halves recursively).
+// The terms are staged in [0, 2^s) of path p's own stage region, which holds only stages below
+// s (dead while the node is pruned) and slot 0 (unused).
+template <int FM>
+__device__ double node_softplus_sum(St& t, int p, int s, int pos, double sg) {
+    const int len = 1 << s;
+    double* T = t.A + p * t.half;
+    for (int j = 0; j < len; ++j) {
+        const double l = fmax(fmin(sg * read_alpha<FM>(t, p, s, pos, j), t.lmax), -t.lmax);
+        T[j] = log(1.0 + exp(-l));
+    }
+    if (len < 8) {
+        double r = 0.0;
+        for (int j = 0; j < len; ++j) r += T[j];
+        return r;
+    }
+    const int blk = len < 128 ? len : 128;
+    double acc[8];  // block sums of the current level, combined pairwise (len is a power of two)
+    double lvl[8];
+    int nl = 0;
+    double total = 0.0;
+    (void)acc;
+    // iterative balanced tree over blocks of 128 (at most 4 blocks at n <= 1024: nb <= 4)
+    const int nb = len / blk;
+    for (int b = 0; b < nb; ++b) {
+        const double* a = T + b * blk;
+        double r[8];
+        for (int j = 0; j < 8; ++j) r[j] = a[j];
+        for (int i = 8; i < blk; i += 8)
+            for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+        lvl[nl++] = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    }
+    while (nl > 1) {
+        for (int i = 0; i < nl / 2; ++i) lvl[i] = lvl[2 * i] + lvl[2 * i + 1];
+        nl /= 2;
+    }
+    total = lvl[0];
+    return total;
+}
+
+// Pruned node (fast-SCL).  Rate-0: pm += node sum (dec.py:269-280).  Repetition: candidates
+// pm + sum(u=0) / pm + sum(u=1) -> selection and fork on the whole node (dec.py:281-306).
+template <int FM>
+__device__ void pruned_node(St& t, int s, int pos, bool rep, int lane) {
+    double pmv = 0.0, pen0 = 0.0, pen1 = 0.0;
+    if (lane < t.L) {
+        pmv = t.pm[lane];
+        pen0 = node_softplus_sum<FM>(t, lane, s, pos, 1.0);
+        if (rep) pen1 = node_softplus_sum<FM>(t, lane, s, pos, -1.0);
+    }
+    __syncthreads();
+    if (!rep) {
+        if (lane < t.L) t.pm[lane] = pmv + pen0;
+        __syncthreads();
+        return;
+    }
+    select_fork(t, pmv, pen0, pen1, pos, 1 << s, lane);
+}
+
+// node type flags of the plan (capi.cpp): bit OFF(s) + (pos >> s), OFF(s) = n - (n >> (s-1))
+__device__ __forceinline__ bool type_bit(const uint32_t* __restrict__ words, int n, int s, int pos) {
+    const int bit = n - (n >> (s - 1)) + (pos >> s);
+    return (words[bit >> 5] >> (bit & 31)) & 1u;
+}
+
+template <int OUTK, int FM, bool FAST>
 __global__ __launch_bounds__(64) void scl_decode_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict__ out,
                                                          double* __restrict__ out_pm,
                                                          const uint32_t* __restrict__ frozen_words,
+                                                         const uint32_t* __restrict__ r0_words,
+                                                         const uint32_t* __restrict__ rep_words,
                                                          const int32_t* __restrict__ info_pos, int n, int log_n, int L,
-                                                         int k, double lmax) {
+                                                         int k, double lmax, int crc_deg, uint32_t crc_g) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const Lay y = make_layout(n, log_n, L);
     const int lane = threadIdx.x;
@@ -250,50 +354,99 @@ __global__ __launch_bounds__(64) void scl_decode_kernel(const float* __restrict_
     if (lane < L) t.pm[lane] = lane == 0 ? 0.0 : lmax;  // :192-194 ([0, 30 x (L-1)] per half)
     __syncthreads();
 
+    // Tree walk in leaf order.  At leaf (or pruned node) start i: combine the nodes that ended
+    // at i-1 above the last finished node (stage `done`), compute the input of the node that
+    // starts at i (g of its parent), then descend with f, pruning rate-0 / repetition nodes.
     const int S = log_n;
-    for (int i = 0; i < n; ++i) {
+    int i = 0, done = 0;
+    while (i < n) {
         int start;
         if (i == 0) {
-            start = S - 1;  // root f is virtual (stage S-1 recomputed from the channel)
+            start = S;  // the root's input is the channel; stage S-1 is virtual (read_alpha)
         } else {
             const int tz = __builtin_ctz(i);
-            for (int s = 1; s <= tz; ++s) combine(t, s, (i - 1) & ~((1 << s) - 1), lane);
-            if (tz + 1 < S) node_fg(t, tz + 1, i & ~((1 << (tz + 1)) - 1), true, lane);
+            for (int s = done + 1; s <= tz; ++s) combine(t, s, (i - 1) & ~((1 << s) - 1), lane);
+            if (tz + 1 < S) node_fg<FM>(t, tz + 1, i & ~((1 << (tz + 1)) - 1), true, lane);
             start = tz;
         }
-        for (int s = start; s >= 1; --s) node_fg(t, s, i & ~((1 << s) - 1), false, lane);
-        const bool info = ((frozen_words[i >> 5] >> (i & 31)) & 1u) == 0u;
-        leaf(t, i, info, lane);
+        int s = start;
+        bool pruned = false;
+        for (; s >= 1; --s) {
+            if constexpr (FAST) {
+                if (type_bit(r0_words, n, s, i)) {
+                    pruned_node<FM>(t, s, i, false, lane);
+                    pruned = true;
+                    break;
+                }
+                if (type_bit(rep_words, n, s, i)) {
+                    pruned_node<FM>(t, s, i, true, lane);
+                    pruned = true;
+                    break;
+                }
+            }
+            if (s < S) node_fg<FM>(t, s, i, false, lane);  // stage S-1 of the root is virtual
+        }
+        if (pruned) {
+            done = s;
+            i += 1 << s;
+        } else {
+            const bool info = ((frozen_words[i >> 5] >> (i & 31)) & 1u) == 0u;
+            leaf<FM>(t, i, info, lane);
+            done = 0;
+            i += 1;
+        }
     }
 
-    // best path: first minimum over states in slot order (sorted msg_pm[:, 0], polar_scl.py:224)
+    // Final sort of the 2L logical rows (row r < L = state r, row r >= L its copy; stable by
+    // pm), CRC penalty per failing row (my_sn dec.py:507-518), first argmin (:224 / :520).
+    __shared__ int fail_s[32];
+    if (lane < L) {
+        int f = 0;
+        if (crc_deg > 0) {
+            const uint32_t* U = t.u + lane * y.W;
+            const uint32_t mask = (1u << crc_deg) - 1u;
+            uint32_t reg = 0;
+            for (int m = 0; m < k; ++m) {
+                const int pos = info_pos[m];
+                const uint32_t fb = ((reg >> (crc_deg - 1)) & 1u) ^ ((U[pos >> 5] >> (pos & 31)) & 1u);
+                reg = (reg << 1) & mask;
+                if (fb) reg ^= crc_g;
+            }
+            f = reg != 0u;
+        }
+        fail_s[lane] = f;
+    }
+    __syncthreads();
     int best = 0;
-    for (int p = 1; p < L; ++p)
-        if (t.pm[p] < t.pm[best]) best = p;
+    {
+        int row[64];
+        for (int r = 0; r < 2 * L; ++r) row[r] = r;
+        for (int a = 1; a < 2 * L; ++a) {
+            const int v = row[a];
+            int c = a - 1;
+            while (c >= 0 && t.pm[row[c] % L] > t.pm[v % L]) {
+                row[c + 1] = row[c];
+                --c;
+            }
+            row[c + 1] = v;
+        }
+        double bestv = 0.0;
+        for (int r = 0; r < 2 * L; ++r) {
+            const int p = row[r] % L;
+            const double v = t.pm[p] + (fail_s[p] ? 30.0 * (double)k : 0.0);
+            if (out_pm != nullptr && lane == 0) out_pm[b * 2 * L + r] = v;
+            if (r == 0 || v < bestv) {
+                best = p;
+                bestv = v;
+            }
+        }
+    }
     const uint32_t* U = t.u + best * y.W;
     for (int m = lane; m < k; m += 64) {
         const int pos = info_pos[m];
         const uint32_t bit = (U[pos >> 5] >> (pos & 31)) & 1u;
         if constexpr (OUTK == PL_OUT_F32) static_cast<float*>(out)[b * k + m] = bit ? 1.0f : 0.0f;
         else static_cast<uint8_t*>(out)[b * k + m] = (uint8_t)bit;
-    }
-    if (out_pm != nullptr && lane == 0) {
-        // final sorted msg_pm: every surviving state appears twice (rows j and j+L)
-        double v[32];
-        for (int p = 0; p < L; ++p) v[p] = t.pm[p];
-        for (int a = 1; a < L; ++a) {
-            const double key = v[a];
-            int c = a - 1;
-            while (c >= 0 && v[c] > key) {
-                v[c + 1] = v[c];
-                --c;
-            }
-            v[c + 1] = key;
-        }
-        for (int p = 0; p < L; ++p) {
-            out_pm[b * 2 * L + 2 * p] = v[p];
-            out_pm[b * 2 * L + 2 * p + 1] = v[p];
-        }
     }
 }
 
@@ -314,18 +467,29 @@ int launch_scl(const pl_plan* p, const float* llr, int64_t bs, void* out, int ou
         set_error("SCL decode: n * list_size too large for LDS");
         return PL_ENOTSUP;
     }
+    const bool fast = (p->flags & PL_PLAN_FAST_SCL) != 0;
+    const bool exact = p->f_mode == PL_F_EXACT;
+    const void* fn = nullptr;
+#define PL_SCL_PICK(O, F, P) if (out_kind == O && (exact ? 1 : 0) == F && fast == P) fn = (const void*)scl_decode_kernel<O, F, P>;
+    PL_SCL_PICK(PL_OUT_F32, 0, false) PL_SCL_PICK(PL_OUT_F32, 0, true) PL_SCL_PICK(PL_OUT_F32, 1, false)
+    PL_SCL_PICK(PL_OUT_F32, 1, true) PL_SCL_PICK(PL_OUT_U8, 0, false) PL_SCL_PICK(PL_OUT_U8, 0, true)
+    PL_SCL_PICK(PL_OUT_U8, 1, false) PL_SCL_PICK(PL_OUT_U8, 1, true)
+#undef PL_SCL_PICK
     if (y.bytes > 64 * 1024) {
-        hipError_t e = out_kind == PL_OUT_F32
-            ? hipFuncSetAttribute((const void*)scl_decode_kernel<PL_OUT_F32>, hipFuncAttributeMaxDynamicSharedMemorySize, y.bytes)
-            : hipFuncSetAttribute((const void*)scl_decode_kernel<PL_OUT_U8>, hipFuncAttributeMaxDynamicSharedMemorySize, y.bytes);
+        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, y.bytes);
         if (e != hipSuccess) return check_hip(e, "SCL decode: LDS attribute");
     }
-    if (out_kind == PL_OUT_F32)
-        hipLaunchKernelGGL(scl_decode_kernel<PL_OUT_F32>, dim3((unsigned)bs), dim3(64), y.bytes, st, llr, bs, out, out_pm,
-                           p->d_frozen_words, p->d_info_pos, p->n, p->log_n, p->list_size, p->k, (double)p->llr_max);
-    else
-        hipLaunchKernelGGL(scl_decode_kernel<PL_OUT_U8>, dim3((unsigned)bs), dim3(64), y.bytes, st, llr, bs, out, out_pm,
-                           p->d_frozen_words, p->d_info_pos, p->n, p->log_n, p->list_size, p->k, (double)p->llr_max);
+    const uint32_t* r0w = p->d_type_words;
+    const uint32_t* repw = p->d_type_words + 2 * p->type_stride;
+    const int32_t* ip = p->d_info_pos;
+    int n = p->n, log_n = p->log_n, L = p->list_size, k = p->k, cdeg = p->crc_deg;
+    double lmax = (double)p->llr_max;
+    uint32_t cg = p->crc_g;
+    const uint32_t* fw = p->d_frozen_words;
+    void* args[] = {(void*)&llr, (void*)&bs, (void*)&out, (void*)&out_pm, (void*)&fw, (void*)&r0w, (void*)&repw,
+                    (void*)&ip, (void*)&n, (void*)&log_n, (void*)&L, (void*)&k, (void*)&lmax, (void*)&cdeg, (void*)&cg};
+    hipError_t e = hipLaunchKernel(fn, dim3((unsigned)bs), dim3(64), args, y.bytes, st);
+    if (e != hipSuccess) return check_hip(e, "SCL decode launch");
     return check_hip(hipGetLastError(), "SCL decode launch");
 }
 }  // namespace pl

@@ -1,0 +1,118 @@
+"""Parity of the my_sn decoder drop-ins on the GPU.
+
+  polar_amd.mysn.SCL_Dec <-> my_sn/fec/polar/dec.py:158-537 (exact f, fast-SCL, CRC-aided pick)
+  polar_amd.mysn.SC_Dec  <-> my_sn/fec/polar/dec.py:13-157  (exact f)
+
+The exact boxplus f is log/exp arithmetic, so the GPU (ocml) and the reference (numpy) differ in
+the last ulp; as for exact-f SC (tests/test_sc_gpu.py) the bits are gated on agreement rate, here
+against both the reference fixtures and the C oracle (glibc), with path metrics within 1e-6 on
+agreeing rows.  The CRC-aided pick and the fast-SCL node sums (numpy pairwise order) are exact
+given the same metrics.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+CASES = [("mysn_scl_L8_32_64", {}), ("mysn_scl_L8_128_256", {}), ("mysn_scl_nofast_L4_32_64", {"fast": False}),
+         ("mysn_scl_crc11_L8_32_64", {"crc": "CRC11"}), ("mysn_scl_crc24c_L8_128_256", {"crc": "CRC24C"})]
+
+
+@pytest.fixture(scope="module")
+def pa():
+    import polar_amd
+    assert torch.cuda.is_available()
+    return polar_amd
+
+
+@pytest.mark.parametrize("fname,kw", CASES, ids=[c[0] for c in CASES])
+def test_mysn_scl_golden(pa, fname, kw):
+    from polar_amd import mysn
+    d = np.load(os.path.join(GOLDEN, fname + ".npz"))
+    n, L = int(d["n"]), int(d["L"])
+    fp = torch.from_numpy(d["frozen_pos"].astype(np.int64))
+    dec = mysn.SCL_Dec(fp, n, list_size=L, use_fast_scl=kw.get("fast", True), crc_degree=kw.get("crc"))
+    rows = agree = 0
+    for name in [k[4:] for k in d.files if k.startswith("llr_")]:
+        x = torch.from_numpy(d["llr_" + name])
+        got = dec(x).numpy().astype(np.uint8)
+        pm = dec.msg_pm
+        ok = (got == d["bits_stable_" + name]).all(1)
+        rows += len(ok)
+        agree += int(ok.sum())
+        assert np.abs(pm[ok] - d["pm_stable_" + name][ok]).max() < 1e-6, name
+    assert agree / rows >= 0.97, (agree, rows)
+
+
+@pytest.mark.parametrize("log_n", [3, 5, 6, 7, 8, 9, 10])
+@pytest.mark.parametrize("L", [2, 8])
+@pytest.mark.parametrize("fast", [True, False])
+def test_mysn_scl_random_vs_oracle(pa, log_n, L, fast):
+    from polar_amd import _lib, ops
+    n = 1 << log_n
+    if n * L > 4096:
+        pytest.skip("oracle time")
+    rng = np.random.default_rng(log_n * 7 + L + fast)
+    k = n // 2
+    fp = np.sort(rng.permutation(n)[: n - k])
+    bs = 37
+    llr = (rng.standard_normal((bs, n)) * 2.5).astype(np.float32)
+    want, wpm = oracle.scl_decode_mysn(llr, fp, L, fast_scl=fast)
+    plan = _lib.Plan(n, pa.frozen_mask(fp, n), L, _lib.PL_F_EXACT, flags=_lib.PL_PLAN_FAST_SCL if fast else 0)
+    got, pm = ops.scl_decode(plan, torch.from_numpy(llr).cuda(), return_pm=True)
+    ok = (got.cpu().numpy() == want).all(1)
+    assert ok.mean() >= 0.95, ok.mean()
+    assert np.abs(pm.cpu().numpy()[ok] - wpm[ok]).max() < 1e-6
+
+
+def test_mysn_scl_minsum_fast_is_exact_vs_oracle(pa):
+    """Fast-SCL with the min-sum f has no transcendental in the tree: bits must be identical."""
+    from polar_amd import _lib, ops
+    for (k, n) in ((32, 64), (128, 256), (512, 1024)):
+        fp = pa.reference_frozen_pos(k, n).numpy()
+        rng = np.random.default_rng(n)
+        llr = (rng.standard_normal((24, n)) * 2 + 1).astype(np.float32)
+        want, wpm = oracle.scl_decode_mysn(llr, fp, 8, fast_scl=True, exact_f=False)
+        plan = _lib.Plan(n, pa.frozen_mask(fp, n), 8, _lib.PL_F_MINSUM, flags=_lib.PL_PLAN_FAST_SCL)
+        got, pm = ops.scl_decode(plan, torch.from_numpy(llr).cuda(), return_pm=True)
+        assert np.array_equal(got.cpu().numpy(), want), (k, n)
+        assert np.abs(pm.cpu().numpy() - wpm).max() < 1e-9
+
+
+def test_mysn_scl_crc_pick_vs_oracle(pa):
+    """CRC-aided pick on CRC-carrying codewords: exact vs the oracle's pick (min-sum f, no
+    transcendental differences), and the CRC raises the block success rate."""
+    from polar_amd import _lib, ops
+    k, n, L = 128, 256, 8
+    fp = pa.reference_frozen_pos(k, n).numpy()
+    info = np.setdiff1d(np.arange(n), fp)
+    rng = np.random.default_rng(9)
+    u = oracle.crc_encode(rng.integers(0, 2, (200, k - 24)).astype(np.float32), "CRC24C")
+    cw = oracle.polar_encode(u, fp, n)
+    llr = ((2 * cw - 1) * 1.6 + rng.standard_normal(cw.shape) * 1.5).astype(np.float32)
+    want, wpm = oracle.scl_decode_mysn(llr, fp, L, fast_scl=True, exact_f=False, crc="CRC24C")
+    plan = _lib.Plan(n, pa.frozen_mask(fp, n), L, _lib.PL_F_MINSUM, flags=_lib.PL_PLAN_FAST_SCL)
+    from polar_amd.mysn import crc_params
+    plan.set_crc(*crc_params("CRC24C"))
+    got, pm = ops.scl_decode(plan, torch.from_numpy(llr).cuda(), return_pm=True)
+    got = got.cpu().numpy()
+    assert np.array_equal(got, want)
+    assert np.abs(pm.cpu().numpy() - wpm).max() < 1e-9
+    plain = _lib.Plan(n, pa.frozen_mask(fp, n), L, _lib.PL_F_MINSUM, flags=_lib.PL_PLAN_FAST_SCL)
+    nocrc = ops.scl_decode(plain, torch.from_numpy(llr).cuda()).cpu().numpy()
+    assert (got == u).all(1).sum() >= (nocrc == u).all(1).sum()
+
+
+def test_mysn_sc_module(pa):
+    from polar_amd import mysn
+    d = np.load(os.path.join(GOLDEN, "sc_128_256.npz"))
+    dec = mysn.SC_Dec(torch.from_numpy(d["frozen_pos"].astype(np.int64)), 256)
+    got = dec(torch.from_numpy(d["llr_awgn2"])).numpy().astype(np.uint8)
+    assert got.shape == d["exact_awgn2"].shape
+    assert (got != d["exact_awgn2"]).any(1).mean() <= 0.02
