@@ -48,6 +48,8 @@ extern "C" {
 
 #define PL_KERNEL_GENERIC 0     /* pl_plan_kernel kinds */
 #define PL_KERNEL_SPECIALIZED 1
+#define PL_KERNEL_SCL_SUBTREE 2 /* SCL plans: lane-per-path register-subtree kernel (default for
+                                   2 <= L <= 32, 32 <= n <= 1024, no fast-SCL pruning) */
 
 #define PL_OUT_F32 0  /* output 0.0f/1.0f floats, [bs, k] (reference output dtype) */
 #define PL_OUT_U8 1   /* output 0/1 bytes, [bs, k] */
@@ -93,7 +95,9 @@ int pl_polar_encode(const pl_plan* plan, const float* u_bits, int64_t bs, float*
  * Call before the plan's first decode.  Replaces SCL_Dec(crc_degree=...) (dec.py:210-218). */
 int pl_plan_set_crc(pl_plan* plan, int32_t degree, uint32_t poly_mask);
 
-/* Which SC kernel a plan launches: *kind = PL_KERNEL_GENERIC / PL_KERNEL_SPECIALIZED; path
+/* Which kernel a plan launches: *kind = PL_KERNEL_GENERIC / PL_KERNEL_SPECIALIZED (SC plans) or
+ * PL_KERNEL_GENERIC / PL_KERNEL_SCL_SUBTREE (SCL plans; PL_PLAN_GENERIC or PL_SCL_TREE=0 in the
+ * environment select the generic SCL kernel); path
  * (nullable) receives the code object file of a specialised kernel. */
 int pl_plan_kernel(const pl_plan* plan, int32_t* kind, char* path, size_t path_len);
 

@@ -18,7 +18,7 @@ PL_OK, PL_EINVAL, PL_EHIP, PL_ENOTSUP = 0, -1, -2, -3
 PL_F_MINSUM, PL_F_EXACT = 0, 1
 PL_OUT_F32, PL_OUT_U8 = 0, 1
 PL_PLAN_GENERIC, PL_PLAN_CACHE_ONLY, PL_PLAN_FAST_SCL = 1, 2, 4
-PL_KERNEL_GENERIC, PL_KERNEL_SPECIALIZED = 0, 1
+PL_KERNEL_GENERIC, PL_KERNEL_SPECIALIZED, PL_KERNEL_SCL_SUBTREE = 0, 1, 2
 
 _lock = threading.Lock()
 _lib = None
@@ -106,10 +106,13 @@ class Plan:
         check(lib().pl_plan_set_crc(self._h, int(degree), int(poly_mask)), "pl_plan_set_crc")
 
     def kernel(self):
-        """('specialized' | 'generic', code-object path or '') of the SC kernel this plan runs."""
+        """(kind, code-object path or '') of the kernel this plan runs: kind is 'specialized' or
+        'generic' for SC plans, 'scl_subtree' or 'generic' for SCL plans."""
         kind, buf = ctypes.c_int32(), ctypes.create_string_buffer(4096)
         check(lib().pl_plan_kernel(self._h, ctypes.byref(kind), buf, 4096), "pl_plan_kernel")
-        return ("specialized" if kind.value == PL_KERNEL_SPECIALIZED else "generic"), buf.value.decode()
+        names = {PL_KERNEL_GENERIC: "generic", PL_KERNEL_SPECIALIZED: "specialized",
+                 PL_KERNEL_SCL_SUBTREE: "scl_subtree"}
+        return names[kind.value], buf.value.decode()
 
     def __del__(self):
         h = getattr(self, "_h", None)

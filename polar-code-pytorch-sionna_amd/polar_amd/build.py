@@ -18,6 +18,11 @@ OBJ = os.path.join(HERE, "_obj")
 LIB = os.path.join(HERE, "libpolar_mi355x.so")
 KCACHE = os.path.join(HERE, "kcache")
 SOURCES = ["sc_kernel.hip", "scl_kernel.hip", "encode_kernel.hip", "capi.cpp", "jit.cpp"]
+# scl_tree_kernel.hip is compiled once per list size (its instantiations, in parallel) and once
+# for the launcher: (object name, source, defines)
+UNITS = [(s + ".o", s, []) for s in SOURCES] + \
+    [(f"scl_tree_L{L}.o", "scl_tree_kernel.hip", [f"-DPL_SCL_TREE_L={L}"]) for L in (2, 4, 8, 16, 32)] + \
+    [("scl_tree_dispatch.o", "scl_tree_kernel.hip", ["-DPL_SCL_TREE_DISPATCH"])]
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 
@@ -55,14 +60,14 @@ def build(force=False, verbose=False):
     deps = [os.path.join(CSRC, "plan.h"),
             os.path.join(HERE, "..", "..", "include", "polar_mi355x.h")]
     jobs = []
-    for s in SOURCES:
+    for oname, s, defs in UNITS:
         src = os.path.join(CSRC, s)
-        obj = os.path.join(OBJ, s + ".o")
+        obj = os.path.join(OBJ, oname)
         extra = [inc] if s == "jit.cpp" else []
         if force or _needs(obj, src, deps + extra):
             lang = ["-x", "hip"] if s.endswith(".cpp") else []
             cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-                   "-ffp-contract=off", f"-I{OBJ}", *lang, "-c", src, "-o", obj]
+                   "-ffp-contract=off", f"-I{OBJ}", *defs, *lang, "-c", src, "-o", obj]
             jobs.append(cmd)
 
     def run(cmd):
@@ -73,7 +78,7 @@ def build(force=False, verbose=False):
             print(r.stdout + r.stderr)
     with ThreadPoolExecutor(max_workers=min(8, len(jobs) or 1)) as ex:
         list(ex.map(run, jobs))
-    objs = [os.path.join(OBJ, s + ".o") for s in SOURCES]
+    objs = [os.path.join(OBJ, u[0]) for u in UNITS]
     if force or jobs or not os.path.exists(LIB):
         cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, f"-L{ROCM}/lib",
                f"-Wl,-rpath,{ROCM}/lib", "-lhiprtc", "-o", LIB]

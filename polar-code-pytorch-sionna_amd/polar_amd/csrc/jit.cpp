@@ -320,7 +320,10 @@ int pl_plan_kernel(const pl_plan* p, int32_t* kind, char* path_out, size_t path_
         pl::set_error("pl_plan_kernel: null plan");
         return PL_EINVAL;
     }
-    if (kind) *kind = p->sc_module ? PL_KERNEL_SPECIALIZED : PL_KERNEL_GENERIC;
+    if (kind) {
+        if (p->list_size > 1) *kind = pl::scl_tree_eligible(p) ? PL_KERNEL_SCL_SUBTREE : PL_KERNEL_GENERIC;
+        else *kind = p->sc_module ? PL_KERNEL_SPECIALIZED : PL_KERNEL_GENERIC;
+    }
     if (path_out && path_len) {
         strncpy(path_out, p->kernel_path.c_str(), path_len - 1);
         path_out[path_len - 1] = 0;

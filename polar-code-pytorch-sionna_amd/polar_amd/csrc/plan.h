@@ -37,6 +37,10 @@ int launch_sc(const pl_plan* plan, const float* llr, int64_t bs, void* out, int 
 size_t scl_workspace_size(const pl_plan* plan, int64_t bs);
 int launch_scl(const pl_plan* plan, const float* llr, int64_t bs, void* out, int out_kind,
                double* out_pm, void* ws, size_t ws_bytes, hipStream_t stream);
+// SCL "register subtree" kernel (scl_tree_kernel.hip); launch_scl dispatches to it when eligible
+bool scl_tree_eligible(const pl_plan* plan);
+int launch_scl_tree(const pl_plan* plan, const float* llr, int64_t bs, void* out, int out_kind, double* out_pm,
+                    hipStream_t stream);
 int launch_encode(const pl_plan* plan, const float* u, int64_t bs, float* cw, hipStream_t stream);
 
 // Code-specialised SC kernels (jit.cpp)

@@ -458,6 +458,7 @@ size_t scl_workspace_size(const pl_plan*, int64_t) { return 0; }
 int launch_scl(const pl_plan* p, const float* llr, int64_t bs, void* out, int out_kind, double* out_pm, void*, size_t,
                hipStream_t st) {
     if (bs == 0) return PL_OK;
+    if (scl_tree_eligible(p)) return launch_scl_tree(p, llr, bs, out, out_kind, out_pm, st);
     if (p->n > 1024) {
         set_error("SCL decode: n must be <= 1024");
         return PL_ENOTSUP;

@@ -28,20 +28,32 @@ def pa():
     return polar_amd
 
 
-def _plan(pa, fp, n, L):
+KERNELS = ["subtree", "generic"]
+
+
+def _plan(pa, fp, n, L, kernel="subtree", f_mode=0):
+    """kernel: 'subtree' = the default SCL kernel (scl_tree_kernel.hip where eligible: 2 <= L,
+    32 <= n), 'generic' = scl_kernel.hip (PL_PLAN_GENERIC)."""
     from polar_amd import _lib
-    return _lib.Plan(n, pa.frozen_mask(fp, n), L, 0)
+    flags = _lib.PL_PLAN_GENERIC if kernel == "generic" else 0
+    p = _lib.Plan(n, pa.frozen_mask(fp, n), L, f_mode, flags=flags)
+    if kernel == "subtree" and L >= 2 and n >= 32:
+        assert p.kernel()[0] == "scl_subtree"
+    elif L > 1:
+        assert p.kernel()[0] == "generic"
+    return p
 
 
 def _sets(d):
     return [k[4:] for k in d.files if k.startswith("llr_")]
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "scl_*.npz"))), ids=os.path.basename)
-def test_scl_golden(pa, path):
+def test_scl_golden(pa, path, kernel):
     d = np.load(path)
     n, L = int(d["n"]), int(d["L"])
-    plan = _plan(pa, d["frozen_pos"], n, L)
+    plan = _plan(pa, d["frozen_pos"], n, L, kernel)
     for name in _sets(d):
         bits, pm = pa.ops.scl_decode(plan, torch.from_numpy(d["llr_" + name]).cuda(), return_pm=True)
         bits = bits.cpu().numpy().astype(np.uint8)
@@ -53,9 +65,10 @@ def test_scl_golden(pa, path):
             assert np.abs(pm - d["pm_" + name]).max() <= PM_TOL, name
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("log_n", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
 @pytest.mark.parametrize("L", [1, 2, 8, 32])
-def test_scl_random_vs_oracle(pa, log_n, L):
+def test_scl_random_vs_oracle(pa, log_n, L, kernel):
     n = 1 << log_n
     if n * L > 32768 or (log_n >= 9 and L == 32):
         pytest.skip("oracle runtime")
@@ -65,9 +78,52 @@ def test_scl_random_vs_oracle(pa, log_n, L):
     bs = 67 if n >= 512 else 131
     llr = (rng.standard_normal((bs, n)) * 2.5 + 0.7).astype(np.float32)
     want_b, want_pm = oracle.scl_decode(llr, fp, L, lazy=True)
-    bits, pm = pa.ops.scl_decode(_plan(pa, fp, n, L), torch.from_numpy(llr).cuda(), return_pm=True)
+    bits, pm = pa.ops.scl_decode(_plan(pa, fp, n, L, kernel), torch.from_numpy(llr).cuda(), return_pm=True)
     assert np.array_equal(bits.cpu().numpy(), want_b)
     assert np.abs(pm.cpu().numpy() - want_pm).max() <= PM_TOL
+
+
+@pytest.mark.parametrize("f_mode", [0, 1])
+@pytest.mark.parametrize("log_n", [5, 6, 7, 8, 9, 10])
+@pytest.mark.parametrize("L", [2, 4, 8, 16, 32])
+def test_scl_subtree_equals_generic(pa, log_n, L, f_mode):
+    """The subtree kernel computes every f, g and metric with the generic kernel's fp64
+    expressions in the same order (both on the GPU, same libm), so bits AND metrics must be
+    identical -- on every list size and length it supports, min-sum and exact f, including
+    exact zeros, integer ties and saturation."""
+    n = 1 << log_n
+    rng = np.random.default_rng(1000 * log_n + L + 7 * f_mode)
+    for k in (n // 4, n // 2, n - 3):
+        fp = np.sort(rng.permutation(n)[: n - k])
+        bs = 96
+        llr = (rng.standard_normal((bs, n)) * 2.5 + 0.5).astype(np.float32)
+        llr[:8] = np.round(llr[:8])
+        llr[8:12] *= 40.0
+        llr[12:14, ::3] = 0.0
+        x = torch.from_numpy(llr).cuda()
+        b1, pm1 = pa.ops.scl_decode(_plan(pa, fp, n, L, "subtree", f_mode), x, return_pm=True)
+        b2, pm2 = pa.ops.scl_decode(_plan(pa, fp, n, L, "generic", f_mode), x, return_pm=True)
+        assert torch.equal(b1, b2), (n, L, k)
+        assert torch.equal(pm1, pm2), (n, L, k)
+
+
+def test_scl_subtree_crc_vs_generic(pa):
+    """CRC-aided pick (pl_plan_set_crc) without fast-SCL runs on the subtree kernel."""
+    from polar_amd.mysn import crc_params
+    k, n, L = 128, 256, 8
+    fp = pa.reference_frozen_pos(k, n).numpy()
+    rng = np.random.default_rng(3)
+    u = oracle.crc_encode(rng.integers(0, 2, (300, k - 11)).astype(np.float32), "CRC11")
+    cw = oracle.polar_encode(u, fp, n)
+    llr = torch.from_numpy(((2 * cw - 1) * 1.5 + rng.standard_normal(cw.shape) * 1.6).astype(np.float32)).cuda()
+    out = []
+    for kernel in KERNELS:
+        p = _plan(pa, fp, n, L, kernel)
+        p.set_crc(*crc_params("CRC11"))
+        out.append(pa.ops.scl_decode(p, llr, return_pm=True))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    want, wpm = oracle.scl_decode_mysn(llr.cpu().numpy(), fp, L, fast_scl=False, exact_f=False, crc="CRC11")
+    assert np.array_equal(out[0][0].cpu().numpy(), want)
 
 
 def test_scl_bench_shape_sample(pa):
