@@ -36,14 +36,26 @@
 
 namespace {
 
-constexpr int R = 5;       // stage of the lane-local subtree
-constexpr int T = 1 << R;  // leaves per lane-local subtree (one partial-sum word)
+// Tuning macros (A/B variants: tools/scl_variants.py)
+#ifndef PL_SCL_R
+#define PL_SCL_R 4  // stage of the lane-local subtree (4 or 5; A/B on MI355X: 4 is 19 % faster)
+#endif
+#ifndef PL_SCL_LOADGRP
+#define PL_SCL_LOADGRP 0  // > 0: stage-R input read in groups of this many pairs (caps VGPRs)
+#endif
+#ifndef PL_SCL_WPE
+#define PL_SCL_WPE 0  // > 0: amdgpu_waves_per_eu minimum
+#endif
+
+constexpr int R = PL_SCL_R;  // stage of the lane-local subtree
+constexpr int T = 1 << R;    // leaves per lane-local subtree (<= one partial-sum word)
 
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
 
 struct Lay {
     int W;    // partial-sum words per path
-    int SS;   // top stored stage (R..SS in LDS); SS == R == S: the channel is the subtree input
+    int SS;   // top stored stage (R..SS in LDS); SS == R == S: the channel is the subtree input,
+              // kept as fp64 in A[0, T) and shared by every path (per = 0)
     int per;  // doubles per path of stored stages
     int off_A, off_ch, off_beta, off_sptr, off_org, off_ps, off_pm, off_fail, bytes;
 };
@@ -54,7 +66,7 @@ __host__ __device__ inline Lay make_layout(int n, int S, int L, int V) {
     y.SS = S == R ? R : S - 1 - V;
     y.per = S == R ? 0 : (1 << (y.SS + 1)) - (1 << R);
     int o = 0;
-    y.off_A = o; o = align16(o + L * y.per * 8);
+    y.off_A = o; o = align16(o + (S == R ? T : L * y.per) * 8);
     y.off_ch = o; o = align16(o + n * 4);
     y.off_beta = o; o = align16(o + L * y.W * 4);
     y.off_sptr = o; o = align16(o + L * (S + 1));
@@ -126,39 +138,99 @@ struct St {
     double lmax;
 };
 
+// Element j + M 2^s of the stage-(s+T) node on the path to the channel, for the stage-s node at
+// pos (D = S - s stages below the channel).  c[m] = channel element j + m 2^s; base[t] =
+// start of the stage-(s+t+1) node + j (g at level t reads bit base[t] + M 2^s of the path).
+template <int D, int T, int M, int FM>
+__device__ __forceinline__ double vtree(const double* c, const uint32_t* bp, const int* base, uint32_t gmask, int hs,
+                                        double lmax) {
+    if constexpr (T == D) {
+        return c[M];
+    } else {
+        const double x = vtree<D, T + 1, M, FM>(c, bp, base, gmask, hs, lmax);
+        const double y = vtree<D, T + 1, M + (1 << T), FM>(c, bp, base, gmask, hs, lmax);
+        if ((gmask >> T) & 1u) return g_op(x, y, getbit(bp, base[T] + M * hs));
+        return f_op<FM>(x, y, lmax);
+    }
+}
+
 // Upper-tree node at stage s (> R), position pos: f (or g) of its input into the stage-(s-1)
-// buffers of every path (s-1 <= SS), wave-parallel over (path, element).
+// buffers of every path (s-1 <= SS), wave-parallel over (path, element).  When the input is
+// virtual (s = SS + 1, V stages below the channel) each lane keeps one element j and loops over
+// the paths, so the 2 x 2^V channel values it needs are read once, not once per path.
 template <int L, int V, int FM>
 __device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane) {
     const int ls = s - 1, h = 1 << ls;
-    const int total = L * h;
-    for (int idx = lane; idx < total; idx += 64) {
-        const int p = idx >> ls, j = idx & (h - 1);
-        const uint32_t* bp = t.beta + p * t.W;
-        double x, y;
-        if (s <= t.SS) {
-            const double* in = t.A + t.sptr[p * (t.S + 1) + s] * t.per + (1 << s) - (1 << R);
-            x = in[j];
-            y = in[j + h];
-        } else {  // s == SS + 1: V stages below the channel
-            x = vread<V, FM>(t.ch, bp, s, pos, j, t.lmax);
-            y = vread<V, FM>(t.ch, bp, s, pos, j + h, t.lmax);
+    if (s <= t.SS || h < 64) {
+        const int total = L * h;
+        for (int idx = lane; idx < total; idx += 64) {
+            const int p = idx >> ls, j = idx & (h - 1);
+            const uint32_t* bp = t.beta + p * t.W;
+            double x, y;
+            if (s <= t.SS) {
+                const double* in = t.A + t.sptr[p * (t.S + 1) + s] * t.per + (1 << s) - (1 << R);
+                x = in[j];
+                y = in[j + h];
+            } else {  // s == SS + 1: V stages below the channel
+                x = vread<V, FM>(t.ch, bp, s, pos, j, t.lmax);
+                y = vread<V, FM>(t.ch, bp, s, pos, j + h, t.lmax);
+            }
+            const double r = is_g ? g_op(x, y, getbit(bp, pos + j)) : f_op<FM>(x, y, t.lmax);
+            t.A[p * t.per + (1 << ls) - (1 << R) + j] = r;
         }
-        const double r = is_g ? g_op(x, y, getbit(bp, pos + j)) : f_op<FM>(x, y, t.lmax);
-        t.A[p * t.per + (1 << ls) - (1 << R) + j] = r;
+    } else {
+        constexpr int NC = 1 << V;
+        const int hs = 1 << s;
+        uint32_t gmask = 0u;  // level t is a g iff the stage-(s+t) node is a right child
+        int bx[V > 0 ? V : 1], by[V > 0 ? V : 1];
+#pragma unroll
+        for (int q = 0; q < V; ++q) {
+            const int st_ = s + q, pp = pos & ~((2 << st_) - 1);
+            if ((pos & ~((1 << st_) - 1)) != pp) gmask |= 1u << q;
+            bx[q] = pp;
+            by[q] = pp + h;
+        }
+        for (int j = lane; j < h; j += 64) {
+            double cx[NC], cy[NC];
+#pragma unroll
+            for (int m = 0; m < NC; ++m) {
+                cx[m] = (double)t.ch[j + m * hs];
+                cy[m] = (double)t.ch[j + h + m * hs];
+            }
+            int basex[V > 0 ? V : 1], basey[V > 0 ? V : 1];
+#pragma unroll
+            for (int q = 0; q < V; ++q) {
+                basex[q] = bx[q] + j;
+                basey[q] = by[q] + j;
+            }
+            for (int p = 0; p < L; ++p) {
+                const uint32_t* bp = t.beta + p * t.W;
+                const double x = vtree<V, 0, 0, FM>(cx, bp, basex, gmask, hs, t.lmax);
+                const double y = vtree<V, 0, 0, FM>(cy, bp, basey, gmask, hs, t.lmax);
+                const double r = is_g ? g_op(x, y, getbit(bp, pos + j)) : f_op<FM>(x, y, t.lmax);
+                t.A[p * t.per + (1 << ls) - (1 << R) + j] = r;
+            }
+        }
     }
     if (lane < L) t.sptr[lane * (t.S + 1) + ls] = (uint8_t)lane;
     __syncthreads();
 }
 
-// beta[pos, pos+h) ^= beta[pos+h, pos+2h) for every path, h = 2^(s-1) >= 32 (word XORs).
+// beta[pos, pos+h) ^= beta[pos+h, pos+2h) for every path, h = 2^(s-1): word XORs for h >= 32,
+// in-word bit ops below.
 template <int L>
-__device__ void combine_words(const St& t, int s, int pos, int lane) {
-    const int hw = 1 << (s - 1 - 5), w0 = pos >> 5;
-    for (int idx = lane; idx < L * hw; idx += 64) {
-        const int p = idx / hw, w = idx - p * hw;
-        uint32_t* b = t.beta + p * t.W;
-        b[w0 + w] ^= b[w0 + hw + w];
+__device__ void combine_upper(const St& t, int s, int pos, int lane) {
+    const int h = 1 << (s - 1);
+    if (h >= 32) {
+        const int hw = h >> 5, w0 = pos >> 5;
+        for (int idx = lane; idx < L * hw; idx += 64) {
+            const int p = idx / hw, w = idx - p * hw;
+            uint32_t* b = t.beta + p * t.W;
+            b[w0 + w] ^= b[w0 + hw + w];
+        }
+    } else if (lane < L) {
+        uint32_t* b = t.beta + lane * t.W + (pos >> 5);
+        *b ^= (*b >> h) & (((1u << h) - 1u) << (pos & 31));
     }
     __syncthreads();
 }
@@ -178,8 +250,14 @@ __device__ __forceinline__ void f_down(double* st, double lmax) {
 }
 
 // stage-R input element j of a lane's subtree (the origin's stored buffer, or the channel)
-__device__ __forceinline__ double in_R(const St& t, const double* inA, int j) {
-    return t.SS == t.S ? (double)t.ch[j] : inA[j];
+__device__ __forceinline__ double in_R(const St&, const double* inA, int j) { return inA[j]; }
+
+__device__ __forceinline__ void load_group_fence(int j) {
+#if PL_SCL_LOADGRP > 0
+    if ((j + 1) % PL_SCL_LOADGRP == 0) __builtin_amdgcn_sched_barrier(0);
+#else
+    (void)j;
+#endif
 }
 
 // Leaf i (> 0) with tz = ctz(i) trailing zeros: g at stage tz+1 into stage tz, then f down.
@@ -198,6 +276,7 @@ __device__ __forceinline__ void g_step(const St& t, const double* inA, double* s
             y = st[IDX(tz + 1) + j + h];
         }
         st[IDX(tz) + j] = g_op(x, y, (ps >> (p0 + j)) & 1u);
+        if constexpr (tz + 1 == R) load_group_fence(j);
     }
     f_down<tz, FM>(st, t.lmax);
 }
@@ -207,7 +286,10 @@ __device__ __forceinline__ void leaf_llr(const St& t, const double* inA, double*
     if (i == 0) {
         constexpr int h = T / 2;
 #pragma unroll
-        for (int j = 0; j < h; ++j) st[IDX(R - 1) + j] = f_op<FM>(in_R(t, inA, j), in_R(t, inA, j + h), t.lmax);
+        for (int j = 0; j < h; ++j) {
+            st[IDX(R - 1) + j] = f_op<FM>(in_R(t, inA, j), in_R(t, inA, j + h), t.lmax);
+            load_group_fence(j);
+        }
         f_down<R - 1, FM>(st, t.lmax);
         return;
     }
@@ -216,7 +298,7 @@ __device__ __forceinline__ void leaf_llr(const St& t, const double* inA, double*
         case 1: g_step<1, FM>(t, inA, st, ps, i); break;
         case 2: g_step<2, FM>(t, inA, st, ps, i); break;
         case 3: g_step<3, FM>(t, inA, st, ps, i); break;
-        default: g_step<4, FM>(t, inA, st, ps, i); break;
+        default: g_step<R - 1, FM>(t, inA, st, ps, i); break;
     }
 }
 
@@ -251,40 +333,42 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
         }
         leaf_llr<FM>(t, inA, st, ps, i);
         const double l = fmax(fmin(st[0], t.lmax), -t.lmax);
-        const double pen0 = log(1.0 + exp(-(1.0 * l)));  // :83, u = 0
-        if ((fz >> i) & 1u) {  // frozen leaf: metric update only
-            pm = pm + pen0;
+        // metric update (:83): pen = log(1 + exp(-(1-2u) l)).  At an information leaf lanes
+        // c >= L (shadows of state c & (L-1)) evaluate u = 1, lanes c < L u = 0: one exp/log per
+        // lane gives all 2L candidates.  Same expression as the reference, so same rounding.
+        const bool info = ((fz >> i) & 1u) == 0u;
+        const bool hi = (lane & L) != 0;
+        const double sl = (info && hi) ? -1.0 * l : 1.0 * l;
+        const double pen = log(1.0 + exp(-sl));
+        if (!info) {  // frozen leaf: metric update only (u = 0)
+            pm = pm + pen;
             continue;
         }
-        const double pen1 = log(1.0 + exp(-(-1.0 * l)));  // u = 1
-        const double c0 = pm + pen0, c1 = pm + pen1;
-        int r0 = 0, r1 = 0;
+        // Lane c < 2L holds candidate c: c < L = (state c, u=0), c >= L = (state c-L, u=1).  Its
+        // rank in the stable (metric, index) order comes from 2L readlane broadcasts; one
+        // ds_permute then sends every candidate to the lane of its rank (ranks are a permutation
+        // of [0, 2L); lanes >= 2L send to themselves, so every lane is written exactly once), and
+        // slots >= L re-shadow slot & (L-1).
+        const double cv = pm + pen;
+        int rk = 0;
 #pragma unroll
-        for (int q = 0; q < L; ++q) {
-            const double a0 = readlane_d(c0, q), a1 = readlane_d(c1, q);
-            r0 += (a0 < c0 || (a0 == c0 && q < lane)) ? 1 : 0;
-            r0 += (a1 < c0) ? 1 : 0;
-            r1 += (a0 <= c1) ? 1 : 0;
-            r1 += (a1 < c1 || (a1 == c1 && q < lane)) ? 1 : 0;
+        for (int c = 0; c < 2 * L; ++c) {
+            const double v = readlane_d(cv, c);
+            rk += (v < cv || (v == cv && c < lane)) ? 1 : 0;
         }
-        int par = 0;
-        uint32_t bit = 0u;
-        double npm = 0.0;
+        const int dst = lane < 2 * L ? rk : lane;
+        const int code = (lane & (L - 1)) | (hi ? 256 : 0);
+        const long long cb = __double_as_longlong(cv);
+        int rcode = __builtin_amdgcn_ds_permute(dst << 2, code);
+        int rlo = __builtin_amdgcn_ds_permute(dst << 2, (int)(cb & 0xffffffffLL));
+        int rhi = __builtin_amdgcn_ds_permute(dst << 2, (int)(cb >> 32));
         const int me = lane & (L - 1);
-#pragma unroll
-        for (int q = 0; q < L; ++q) {
-            const int q0 = __builtin_amdgcn_readlane(r0, q), q1 = __builtin_amdgcn_readlane(r1, q);
-            if (q0 == me) {
-                par = q;
-                bit = 0u;
-                npm = readlane_d(c0, q);
-            }
-            if (q1 == me) {
-                par = q;
-                bit = 1u;
-                npm = readlane_d(c1, q);
-            }
-        }
+        rcode = bperm_i(rcode, me);
+        rlo = bperm_i(rlo, me);
+        rhi = bperm_i(rhi, me);
+        const int par = rcode & 255;
+        const uint32_t bit = (uint32_t)rcode >> 8;
+        const double npm = __longlong_as_double(((long long)rhi << 32) | (unsigned int)rlo);
         pm = npm;
         ps = (uint32_t)bperm_i((int)ps, par) | (bit << i);
         org = bperm_i(org, par);
@@ -298,7 +382,11 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
 }
 
 template <int L, int V, int FM>
-__global__ __launch_bounds__(64) void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict__ out,
+__global__ __launch_bounds__(64)
+#if PL_SCL_WPE > 0
+__attribute__((amdgpu_waves_per_eu(PL_SCL_WPE)))
+#endif
+void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict__ out,
                                                       int out_kind, double* __restrict__ out_pm,
                                                       const uint32_t* __restrict__ frozen_words,
                                                       const int32_t* __restrict__ info_pos, int n, int S, int k,
@@ -333,6 +421,8 @@ __global__ __launch_bounds__(64) void scl_tree_kernel(const float* __restrict__ 
     }
     for (int i = lane; i < L * y.W; i += 64) t.beta[i] = 0u;
     for (int i = lane; i < L * (S + 1); i += 64) t.sptr[i] = (uint8_t)(i / (S + 1));
+    if (S == R)  // the whole tree is one lane-local subtree: its input is the channel, as fp64
+        for (int i = lane; i < T; i += 64) t.A[i] = (double)t.ch[i];
     __syncthreads();
 
     double pm = (lane & (L - 1)) == 0 ? 0.0 : lmax;  // :192-194 ([0, 30 x (L-1)] per half)
@@ -352,7 +442,7 @@ __global__ __launch_bounds__(64) void scl_tree_kernel(const float* __restrict__ 
         }
         int org;
         uint32_t ps;
-        subtree<L, FM>(t, i0, frozen_words[i0 >> 5], pm, org, ps, lane);
+        subtree<L, FM>(t, i0, frozen_words[i0 >> 5] >> (i0 & 31), pm, org, ps, lane);
         // re-point the upper-tree state of every path to its origin's, then store the
         // subtree's partial sums: partial-sum words before i0 and stage owners R..SS
         if (lane < L) {
@@ -360,14 +450,14 @@ __global__ __launch_bounds__(64) void scl_tree_kernel(const float* __restrict__ 
             t.ps_s[lane] = ps;
         }
         __syncthreads();
-        const int w_i = i0 >> 5;
+        const int w_i = i0 >> 5, w_lim = (i0 + 31) >> 5, off = i0 & 31;
         constexpr int RB = (L * 32 + 63) / 64;  // <= L*W/64 words per lane (n <= 1024)
         uint32_t vb[RB];
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
             const int idx = r * 64 + lane;
             const int np = idx >> 5, w = idx & 31;
-            if (np < L && w < w_i) vb[r] = t.beta[t.org_s[np] * y.W + w];
+            if (np < L && w < w_lim) vb[r] = t.beta[t.org_s[np] * y.W + w];
         }
         constexpr int RS = (L * 11 + 63) / 64;
         uint8_t vs[RS];
@@ -382,19 +472,23 @@ __global__ __launch_bounds__(64) void scl_tree_kernel(const float* __restrict__ 
         for (int r = 0; r < RB; ++r) {
             const int idx = r * 64 + lane;
             const int np = idx >> 5, w = idx & 31;
-            if (np < L && w < w_i) t.beta[np * y.W + w] = vb[r];
+            if (np < L && w < w_lim) t.beta[np * y.W + w] = vb[r];
         }
 #pragma unroll
         for (int r = 0; r < RS; ++r) {
             const int idx = r * 64 + lane;
             if (idx < L * S1) t.sptr[idx] = vs[r];
         }
-        if (lane < L) t.beta[lane * y.W + w_i] = ps;
+        if (T < 32 && off != 0) __syncthreads();  // the word's low part was just copied
+        if (lane < L) {
+            uint32_t* bw = t.beta + lane * y.W + w_i;
+            *bw = off == 0 ? ps : ((*bw & ((1u << off) - 1u)) | (ps << off));
+        }
         __syncthreads();
         // nodes above R that end with this subtree
         const int nxt = i0 + T;
         const int top = nxt < n ? __builtin_ctz(nxt) : S;
-        for (int s = R + 1; s <= top; ++s) combine_words<L>(t, s, nxt - (1 << s), lane);
+        for (int s = R + 1; s <= top; ++s) combine_upper<L>(t, s, nxt - (1 << s), lane);
     }
     if (lane < L) pm_s[lane] = pm;
 
@@ -512,7 +606,7 @@ bool scl_tree_eligible(const pl_plan* p) {
     if (p->flags & (PL_PLAN_FAST_SCL | PL_PLAN_GENERIC)) return false;
     if (const char* e = getenv("PL_SCL_TREE"))
         if (e[0] == '0') return false;
-    return p->list_size >= 2 && p->list_size <= 32 && p->log_n >= R && p->log_n <= 10;
+    return p->list_size >= 2 && p->list_size <= 32 && p->log_n >= 5 && p->log_n <= 10;
 }
 
 int launch_scl_tree(const pl_plan* p, const float* llr, int64_t bs, void* out, int out_kind, double* out_pm,
@@ -525,6 +619,13 @@ int launch_scl_tree(const pl_plan* p, const float* llr, int64_t bs, void* out, i
     const int S = p->log_n, L = p->list_size, V = pick_v(S);
     const bool exact = p->f_mode == PL_F_EXACT;
     const void* fn = nullptr;
+#ifdef PL_SCL_VARIANT_ONLY_L8  // development variant libraries (tools/scl_variants.py)
+    if (L != 8) {
+        set_error("variant library: L = 8 only");
+        return PL_ENOTSUP;
+    }
+    fn = scl_tree_fn<8>(V, exact);
+#else
     switch (L) {
         case 2: fn = scl_tree_fn<2>(V, exact); break;
         case 4: fn = scl_tree_fn<4>(V, exact); break;
@@ -532,6 +633,7 @@ int launch_scl_tree(const pl_plan* p, const float* llr, int64_t bs, void* out, i
         case 16: fn = scl_tree_fn<16>(V, exact); break;
         default: fn = scl_tree_fn<32>(V, exact); break;
     }
+#endif
     const Lay y = make_layout(p->n, S, L, V);
     if (y.bytes > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, y.bytes);

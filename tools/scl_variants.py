@@ -1,0 +1,94 @@
+"""Development aid: build SCL subtree-kernel variants (-D flags, L = 8 only) and time them in ONE
+process on the GPU against the default library.
+
+  python tools/scl_variants.py build NAME:"-DPL_SCL_R=4" ...     (build container; hipcc)
+  python tools/scl_variants.py time [--n 1024 --k 512 --bs 8192]   (GPU box)
+Variant libraries go to polar-code-pytorch-sionna_amd/polar_amd/_variants/ (git-ignored).
+Environment knobs read at launch (PL_SCL_VIRTUAL=<max virtual stages>) apply to every library.
+"""
+import ctypes
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "polar-code-pytorch-sionna_amd")
+VAR = os.path.join(PKG, "polar_amd", "_variants")
+sys.path.insert(0, PKG)
+
+
+def build(specs):
+    from polar_amd import build as b
+    b.build()
+    os.makedirs(VAR, exist_ok=True)
+    hipcc = b._hipcc()
+    objs = [os.path.join(b.OBJ, u[0]) for u in b.UNITS if u[1] != "scl_tree_kernel.hip"]
+
+    def one(spec):
+        name, flags = spec.split(":", 1)
+        base = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", *flags.split()]
+        src = os.path.join(b.CSRC, "scl_tree_kernel.hip")
+        o1, o2 = os.path.join(VAR, f"sclt_{name}_L8.o"), os.path.join(VAR, f"sclt_{name}_disp.o")
+        subprocess.check_call(base + ["-DPL_SCL_TREE_L=8", "-c", src, "-o", o1])
+        subprocess.check_call(base + ["-DPL_SCL_TREE_DISPATCH", "-DPL_SCL_VARIANT_ONLY_L8", "-c", src, "-o", o2])
+        subprocess.check_call([hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", o1, o2, *objs,
+                               f"-L{b.ROCM}/lib", f"-Wl,-rpath,{b.ROCM}/lib", "-lhiprtc",
+                               "-o", os.path.join(VAR, f"libscl_{name}.so")])
+        return name
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(4) as ex:
+        print(list(ex.map(one, specs)))
+
+
+def time_all(n=1024, k=512, bs=8192, reps=5, rounds=2):
+    import numpy as np
+    import torch
+    import polar_amd
+    from polar_amd import _lib
+    libs = [("default", _lib.LIB_PATH)] + [(f[7:-3], os.path.join(VAR, f)) for f in sorted(os.listdir(VAR))
+                                           if f.startswith("libscl_") and f.endswith(".so")]
+    fp = polar_amd.reference_frozen_pos(k, n).numpy()
+    mask = np.ascontiguousarray(polar_amd.frozen_mask(fp, n), dtype=np.uint8)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    llr = torch.randn((bs, n), device="cuda", generator=g) * 2.5 + 1.0
+    ref = None
+    handles = []
+    for name, path in libs:
+        L = _lib._declare(ctypes.CDLL(path))
+        h = ctypes.c_void_p()
+        assert L.pl_plan_create(ctypes.byref(h), n, mask.ctypes.data_as(ctypes.c_void_p), 8, 0, 30.0, 0) == 0
+        handles.append((name, L, h))
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for rnd in range(rounds):
+        for name, L, h in handles:
+            out = torch.empty((bs, k), device="cuda")
+            pm = torch.empty((bs, 16), device="cuda", dtype=torch.float64)
+            call = lambda: L.pl_scl_decode(h, ctypes.c_void_p(llr.data_ptr()), bs, ctypes.c_void_p(out.data_ptr()),  # noqa
+                                           0, ctypes.c_void_p(pm.data_ptr()), None, 0, stream)
+            assert call() == 0, L.pl_last_error_string()
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(reps):
+                call()
+            e.record()
+            torch.cuda.synchronize()
+            ms = s.elapsed_time(e) / reps
+            if ref is None:
+                ref = (out.clone(), pm.clone())
+            same = torch.equal(out, ref[0]) and torch.equal(pm, ref[1])
+            print(f"round {rnd} {name:16s} {ms:8.3f} ms  {bs / ms / 1e3:7.4f} Mcw/s  identical={same}", flush=True)
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "build":
+        build(sys.argv[2:])
+    else:
+        import argparse
+        ap = argparse.ArgumentParser()
+        ap.add_argument("cmd")
+        ap.add_argument("--n", type=int, default=1024)
+        ap.add_argument("--k", type=int, default=512)
+        ap.add_argument("--bs", type=int, default=8192)
+        a = ap.parse_args()
+        time_all(a.n, a.k, a.bs)
