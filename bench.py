@@ -40,13 +40,15 @@ def parse():
                     help="untimed launches before the warmup steps so the GPU clock leaves its idle state")
     ap.add_argument("--k", type=int, default=512)
     ap.add_argument("--n", type=int, default=1024)
-    ap.add_argument("--bs", type=int, default=65536, help="codewords per GPU")
+    ap.add_argument("--bs", type=int, default=None, help="codewords per GPU (default 65536 SC / 8192 SCL)")
     ap.add_argument("--ebno", type=float, default=2.0)
     ap.add_argument("--decoder", choices=["sc", "scl"], default="sc")
     ap.add_argument("--list-size", type=int, default=8)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     a = ap.parse_args()
+    if a.bs is None:
+        a.bs = 65536 if a.decoder == "sc" else 8192  # BASELINE.json configs[2] / configs[3]
     if a.steps is None:
         a.steps = 1000 if a.decoder == "sc" else 20
     if a.warmup is None:
@@ -188,7 +190,7 @@ def main():
             "config": {"workload": f"{a.decoder.upper()} decode (k={k}, n={n}), bs={bs} per GPU"
                                    + (f", L={L}" if L > 1 else ""),
                        "k": k, "n": n, "bs_per_gpu": bs, "global_batch": bs * world,
-                       "kernel": plan.kernel()[0] if a.decoder == "sc" else "scl",
+                       "kernel": plan.kernel()[0],
                        "parallelism": f"dp{world}"},
             "info_gbit_s": round(total_cw * k / wall / 1e9, 4),
             "bler": round(float(blk[0].item()) / float(blk[1].item()), 6),

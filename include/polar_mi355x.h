@@ -19,6 +19,10 @@
  *                    (+ final sorted msg_pm of _decode_np_batch :178-209)
  *   pl_polar_encode  PolarEncoder.forward x_run_sn_polar/polar/enc.py:30-43
  *                    (butterfly form of my_sn/fec/polar/enc.py:85-96)
+ *   pl_crc_attach    CRCEncoder.forward my_sn/fec/crc.py:85-104 (G-matrix CRC, 5G polynomials :38-52)
+ *   pl_gather_rows   Polar5GEncoder.forward rate matching c[:, ind_rate_matching]
+ *                    my_sn/fec/polar/enc.py:378-392
+ *   pl_rate_recover  Polar5GDecoder.forward rate recovery my_sn/fec/polar/dec.py:621-654
  *   pl_plan_kernel / pl_sc_specialize: no reference counterpart (kernel specialisation per
  *                    frozen set, the tree walk of polar_sc.py:54-98 resolved at compile time)
  */
@@ -106,6 +110,22 @@ int pl_plan_kernel(const pl_plan* plan, int32_t* kind, char* path, size_t path_l
  * kernels of known codes. */
 int pl_sc_specialize(int32_t n, const uint8_t* frozen_mask, int32_t f_mode, const char* cache_dir,
                      char* path, size_t path_len);
+
+/* 5G NR data path (polar_amd/polar5g.py builds the tables on the host, 3GPP TS 38.212 5.4.1).
+ * All pointers are device pointers; rows are contiguous fp32.
+ * pl_crc_attach:   out[b] = [u[b], parity(u[b])], parity bit c = XOR of g_rows[m] bit c over the
+ *                  1 bits m of u[b] (g_rows: k generator rows, bit c = parity column c; degree <= 32).
+ * pl_gather_rows:  out[b, j] = in[b, idx[j]], j < n_out <= 4096 (rate matching).
+ * pl_rate_recover: out[b, j] = src_a[j] < 0 ? fill[j] : in[b, src_a[j]] (+ in[b, src_b[j]] if
+ *                  src_b (nullable) has src_b[j] >= 0), j < n <= 2048 (de-interleaving, puncturing
+ *                  = fill 0, shortening = fill -llr_max, repetition = the sum, sub-block
+ *                  de-interleaving folded into one table). */
+int pl_crc_attach(const float* u, int64_t bs, int32_t k, const uint32_t* g_rows, int32_t degree, float* out,
+                  void* hip_stream);
+int pl_gather_rows(const float* in, int64_t bs, int32_t n_in, const int32_t* idx, int32_t n_out, float* out,
+                   void* hip_stream);
+int pl_rate_recover(const float* llr, int64_t bs, int32_t e, const int32_t* src_a, const int32_t* src_b,
+                    const float* fill, int32_t n, float* out, void* hip_stream);
 
 const char* pl_last_error_string(void);
 const char* pl_version(void);

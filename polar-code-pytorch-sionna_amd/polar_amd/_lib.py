@@ -41,10 +41,14 @@ def _declare(L):
     L.pl_plan_kernel.argtypes = [P, P, ctypes.c_char_p, ctypes.c_size_t]
     L.pl_plan_set_crc.argtypes = [P, i32, u32]
     L.pl_sc_specialize.argtypes = [i32, P, i32, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
+    L.pl_crc_attach.argtypes = [P, i64, i32, P, i32, P, P]
+    L.pl_gather_rows.argtypes = [P, i64, i32, P, i32, P, P]
+    L.pl_rate_recover.argtypes = [P, i64, i32, P, P, P, i32, P, P]
     L.pl_last_error_string.restype = ctypes.c_char_p
     L.pl_version.restype = ctypes.c_char_p
     for f in (L.pl_plan_create, L.pl_plan_destroy, L.pl_plan_info, L.pl_sc_decode, L.pl_scl_decode,
-              L.pl_polar_encode, L.pl_plan_kernel, L.pl_sc_specialize, L.pl_plan_set_crc):
+              L.pl_polar_encode, L.pl_plan_kernel, L.pl_sc_specialize, L.pl_plan_set_crc, L.pl_crc_attach,
+              L.pl_gather_rows, L.pl_rate_recover):
         f.restype = ctypes.c_int
     return L
 
@@ -65,8 +69,8 @@ def lib():
 
 EXPORTED_SYMBOLS = ("pl_plan_create", "pl_plan_destroy", "pl_plan_info", "pl_sc_decode",
                     "pl_scl_workspace_size", "pl_scl_decode", "pl_polar_encode",
-                    "pl_plan_kernel", "pl_sc_specialize", "pl_plan_set_crc", "pl_last_error_string",
-                    "pl_version")
+                    "pl_plan_kernel", "pl_sc_specialize", "pl_plan_set_crc", "pl_crc_attach", "pl_gather_rows",
+                    "pl_rate_recover", "pl_last_error_string", "pl_version")
 
 
 def check(rc, what):

@@ -17,7 +17,7 @@ CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "_obj")
 LIB = os.path.join(HERE, "libpolar_mi355x.so")
 KCACHE = os.path.join(HERE, "kcache")
-SOURCES = ["sc_kernel.hip", "scl_kernel.hip", "encode_kernel.hip", "capi.cpp", "jit.cpp"]
+SOURCES = ["sc_kernel.hip", "scl_kernel.hip", "encode_kernel.hip", "ratematch_kernel.hip", "capi.cpp", "jit.cpp"]
 # scl_tree_kernel.hip is compiled once per list size (its instantiations, in parallel) and once
 # for the launcher: (object name, source, defines)
 UNITS = [(s + ".o", s, []) for s in SOURCES] + \
@@ -123,9 +123,30 @@ def prebuild_codes(codes, workers=None, prune=True):
                 os.remove(os.path.join(KCACHE, f))
 
 
+# 5G NR (k, E) configurations the package's tests decode (tests/test_polar5g_gpu.py); their
+# mother codes are decoded by the exact-f SC kernel (Polar5GDecoder dec_type="SC")
+POLAR5G_TEST_CODES = [(12, 20), (12, 160), (16, 64), (19, 100), (20, 40), (24, 300), (32, 64), (40, 100), (48, 64),
+                      (64, 128), (64, 200), (100, 180), (120, 1000), (140, 576), (200, 400), (250, 300),
+                      (300, 1088), (500, 1024), (512, 700), (1013, 1088), (30, 1088), (64, 1024)]
+
+
+def polar5g_codes():
+    """Exact-f SC codes of the 5G mother codes in POLAR5G_TEST_CODES (uplink)."""
+    import numpy as np
+    from .polar5g import _rate_match_tables
+    out = []
+    for k, e in POLAR5G_TEST_CODES:
+        _, n_polar, frozen, _, _ = _rate_match_tables(k, e, "uplink")
+        m = np.zeros(n_polar, dtype=np.uint8)
+        m[np.asarray(frozen, dtype=np.int64)] = 1
+        out.append((m, 1))
+    return out
+
+
 def reference_codes():
     """The codes the reference harness and this package's tests/bench use: every pinned
-    reference frozen set with n <= 2048 (min-sum), and the golden shapes in exact-f mode."""
+    reference frozen set with n <= 2048 (min-sum), the golden shapes in exact-f mode, and the
+    5G mother codes the tests decode (exact f)."""
     import numpy as np
     data = os.path.join(HERE, "data", "frozen_sets.npz")
     out = []
@@ -140,7 +161,14 @@ def reference_codes():
             if (k, n) in ((2, 4), (4, 8), (8, 16), (16, 32), (16, 64), (32, 64), (48, 64), (128, 256),
                           (256, 512), (512, 1024), (1024, 2048)):
                 out.append((m, 1))
-    return out
+    import contextlib
+    import io
+    with contextlib.redirect_stdout(io.StringIO()):  # the CRC6 warning of 12 <= k <= 19
+        out += polar5g_codes()
+    uniq = {}
+    for m, fm in out:
+        uniq[(bytes(bytearray(m)), fm)] = (m, fm)
+    return list(uniq.values())
 
 
 if __name__ == "__main__":
