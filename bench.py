@@ -73,14 +73,16 @@ def cpu_baseline(llr_host, fp, k, n, decoder, L, budget_s):
     while True:
         fn(sample)
         done += len(sample)
-        if time.perf_counter() - t0 >= budget_s or done >= 64 * len(sample):
+        if time.perf_counter() - t0 >= budget_s or (decoder == "sc" and done >= 64 * len(sample)):
             break
     dt = time.perf_counter() - t0
     return {"value": round(done / dt / 1e6, 6), "unit": "Mcodewords/s", "cores": threads, "kind": "port",
             "sample": f"{done} codewords ({len(sample)}-codeword batches of the same AWGN LLRs, "
                       f"(k={k},n={n}) {decoder.upper()}, oracle/polar_oracle.c OpenMP) in {dt:.1f} s",
-            "reference_cpu_note": "reference x_run SC_Dec measured in the build container (8 Xeon "
-                                  "threads): 0.00603 Mcodewords/s at this shape (BASELINE.md §2)"}
+            "reference_cpu_note": ("reference x_run SC_Dec measured in the build container (8 Xeon "
+                                   "threads): 0.00603 Mcodewords/s at this shape (BASELINE.md §2)") if decoder == "sc"
+            else ("reference x_run SCL_Dec (L=8) measured in the build container (8 Xeon threads): "
+                  "6.15e-06 Mcodewords/s at n=1024 (BASELINE.md §2)")}
 
 
 def traffic_from_profiles(tag):

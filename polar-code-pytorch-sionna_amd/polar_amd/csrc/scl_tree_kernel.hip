@@ -2,27 +2,32 @@
 //
 // Same decoder as scl_kernel.hip (x_run_sn_polar/polar/polar_scl.py SCL_Dec, :49-234; and the
 // exact-f variant of my_sn/fec/polar/dec.py:330-339 without fast-SCL pruning), restructured for
-// latency: the reference walks the tree leaf by leaf with a sort + full-row copy of all 2L paths
-// at every information leaf (:86-120); here
+// latency and lane utilisation: the reference walks the tree leaf by leaf with a sort + full-row
+// copy of all 2L paths at every information leaf (:86-120); here
 //
-//  * the bottom of the tree runs LANE-PER-PATH: lane p (< L) decodes path p's stage-R node
-//    (R = 5, 32 leaves) entirely in its VGPRs -- stage buffers 0..R-1 (31 fp64), the node's
-//    partial sums as one bit word, the path metric.  f/g, the per-leaf metric update
-//    (:69-85) and, at information leaves, the 2L-candidate selection (:86-92) run without LDS
-//    traffic: candidates are ranked by v_readlane broadcasts (stable (metric, candidate index)
-//    order, candidate c < L = (state c, u=0), c >= L = (state c-L, u=1) -- the reference's
-//    logical order after _update_single_bit_np :49-68), and a fork (:109-120) pulls the parent's
-//    LIVE stage buffers with ds_bpermute (a stage-s buffer is live iff the leaf is in the left
-//    half of its stage-s node; dead ones are never copied);
+//  * one wave decodes CPW = 64 / 2L codewords; codeword c owns the 2L-lane group
+//    [2Lc, 2Lc + 2L): lanes 0..L-1 of the group are its paths, lanes L..2L-1 shadow them and
+//    evaluate the u = 1 candidates, so every lane of the wave does useful work at the leaves;
+//  * the bottom of the tree runs LANE-PER-PATH: a path lane decodes its path's stage-R node
+//    (R = 4, 16 leaves) entirely in its VGPRs -- stage buffers 0..R-1 (fp64), the node's
+//    partial sums as one bit word, the path metric.  f/g, the per-leaf metric update (:69-85)
+//    and, at information leaves, the 2L-candidate selection (:86-92) run without LDS traffic:
+//    candidates are ranked in the group by DPP row rotations (2L = 16), quad permutes (2L = 4),
+//    ds_bpermute (2L = 8, 32) or readlane (2L = 64), in the stable (metric, candidate index)
+//    order -- candidate c < L = (state c, u=0), c >= L = (state c-L, u=1), the reference's
+//    logical order after _update_single_bit_np :49-68 -- and a fork (:109-120) pulls the
+//    parent's LIVE stage buffers with ds_bpermute (a stage-s buffer is live iff the leaf is in
+//    the left half of its stage-s node; dead ones are never copied);
 //  * forks only move register state: each lane records the path it descends from at subtree
 //    entry ("origin"); the LDS state of the upper tree (stage-buffer owner pointers, partial
 //    sums of finished nodes) is re-pointed once per subtree, from the origins, instead of once
 //    per information leaf;
-//  * the upper stages run WAVE-PARALLEL over (path, element) from LDS, with lazy copies (per
-//    path per stage owner pointers, as scl_kernel.hip);
-//  * the top V stages below the channel are never stored: a node reading one recomputes its
-//    input from the channel and the path's partial sums (f/g are pure functions of those), so a
-//    codeword needs ~11 KB of LDS at n=1024, L=8 (14 codewords per CU instead of 4);
+//  * the upper stages run WAVE-PARALLEL over (codeword, path, element) from LDS, with lazy
+//    copies (per path per stage owner pointers, as scl_kernel.hip);
+//  * the channel is never copied to LDS, and the top V stages below it are never stored: a node
+//    reading one recomputes its input from the channel row in global memory (L2-resident after
+//    the first pass) and the path's partial sums (f/g are pure functions of those), so a
+//    codeword needs ~4.5 KB of LDS at n=1024, L=8, V=4;
 //  * decided bits are not tracked: the root's partial sums are x = u G_n and u = x G_n (G_n is
 //    an involution over GF(2)), recovered by one butterfly per path at the end.
 //
@@ -44,20 +49,22 @@ namespace {
 #define PL_SCL_LOADGRP 0  // > 0: stage-R input read in groups of this many pairs (caps VGPRs)
 #endif
 #ifndef PL_SCL_WPE
-#define PL_SCL_WPE 0  // > 0: amdgpu_waves_per_eu minimum
+#define PL_SCL_WPE 2  // > 0: amdgpu_waves_per_eu minimum (2: <= 256 VGPRs, A/B on MI355X: 2.30 vs 3.62 ms at V=4)
 #endif
 
 constexpr int R = PL_SCL_R;  // stage of the lane-local subtree
 constexpr int T = 1 << R;    // leaves per lane-local subtree (<= one partial-sum word)
 
+__host__ __device__ constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x >> 1); }
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
 
+// LDS layout of ONE codeword; codeword c of a wave sits at c * bytes.
 struct Lay {
     int W;    // partial-sum words per path
     int SS;   // top stored stage (R..SS in LDS); SS == R == S: the channel is the subtree input,
               // kept as fp64 in A[0, T) and shared by every path (per = 0)
     int per;  // doubles per path of stored stages
-    int off_A, off_ch, off_beta, off_sptr, off_org, off_ps, off_pm, off_fail, bytes;
+    int off_A, off_beta, off_sptr, off_org, off_ps, off_pm, off_fail, off_sv, off_sp, bytes;
 };
 
 __host__ __device__ inline Lay make_layout(int n, int S, int L, int V) {
@@ -67,13 +74,14 @@ __host__ __device__ inline Lay make_layout(int n, int S, int L, int V) {
     y.per = S == R ? 0 : (1 << (y.SS + 1)) - (1 << R);
     int o = 0;
     y.off_A = o; o = align16(o + (S == R ? T : L * y.per) * 8);
-    y.off_ch = o; o = align16(o + n * 4);
     y.off_beta = o; o = align16(o + L * y.W * 4);
     y.off_sptr = o; o = align16(o + L * (S + 1));
     y.off_org = o; o = align16(o + L * 4);
     y.off_ps = o; o = align16(o + L * 4);
     y.off_pm = o; o = align16(o + L * 8);
     y.off_fail = o; o = align16(o + L * 4);
+    y.off_sv = o; o = align16(o + 2 * L * 8);  // final: metric + penalty of sorted row r
+    y.off_sp = o; o = align16(o + 2 * L * 4);  // final: state of sorted row r
     y.bytes = o;
     return y;
 }
@@ -112,71 +120,131 @@ __device__ __forceinline__ double bperm_d(double v, int src) {
     const int hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)(b >> 32));
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffffLL), CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, true);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
 
-// Element j of the stage-s node at position pos of one path, D stages below the channel,
-// recomputed from the channel and the path's partial sums (virtual stages).
-template <int D, int FM>
-__device__ __forceinline__ double vread(const float* ch, const uint32_t* beta, int s, int pos, int j, double lmax) {
-    if constexpr (D == 0) {
-        return (double)ch[j];
-    } else {
-        const int h = 1 << s, pp = pos & ~(2 * h - 1);
-        const double x = vread<D - 1, FM>(ch, beta, s + 1, pp, j, lmax);
-        const double y = vread<D - 1, FM>(ch, beta, s + 1, pp, j + h, lmax);
-        return pos == pp ? f_op<FM>(x, y, lmax) : g_op(x, y, getbit(beta, pp + j));
+// Candidate (metric) of group lane (gl + r) mod GW, r = 1..GW-1, accumulated into the rank of
+// this lane's candidate in the stable (metric, index) order.
+template <int GW, int r>
+__device__ __forceinline__ void rank_rot(double cv, int gl, int lane, int& rk) {
+    if constexpr (r < GW) {
+        double v;
+        if constexpr (GW == 16) {
+            v = dpp_d<0x120 + r>(cv);  // row_ror:r -- the 16-lane DPP row is the group
+        } else if constexpr (GW == 4) {
+            constexpr int q = ((0 + r) & 3) | (((1 + r) & 3) << 2) | (((2 + r) & 3) << 4) | (((3 + r) & 3) << 6);
+            v = dpp_d<q>(cv);  // quad_perm rotation
+        } else {
+            v = bperm_d(cv, (lane & ~(GW - 1)) | ((gl + r) & (GW - 1)));
+        }
+        // source group lane of the rotation (DPP row_ror / quad_perm / bpermute), moved like
+        // the value so the direction convention cannot matter
+        int ci;
+        if constexpr (GW == 16) ci = __builtin_amdgcn_mov_dpp(gl, 0x120 + r, 0xF, 0xF, true);
+        else ci = (gl + r) & (GW - 1);
+        rk += (v < cv || (v == cv && ci < gl)) ? 1 : 0;
+        rank_rot<GW, r + 1>(cv, gl, lane, rk);
     }
 }
 
-struct St {
+// One codeword's state: LDS regions and its channel row.
+struct Cw {
     double* A;        // [L][per] stage s (R <= s <= SS) of buffer b at A[b*per + 2^s - 2^R + j]
-    float* ch;        // [n] negated channel LLRs (stage S)
     uint32_t* beta;   // [L][W] partial sums by absolute position
     uint8_t* sptr;    // [L][S+1] owner buffer of stage s
     int* org_s;       // [L] subtree exchange: origin path
     uint32_t* ps_s;   // [L] subtree exchange: partial-sum word
-    int n, S, W, SS, per;
-    double lmax;
+    double* pm_s;     // [L] final metrics
+    int* fail_s;      // [L] CRC failure flags
+    double* sv;       // [2L] final sorted values
+    int* sp;          // [2L] final sorted states
+    const float* ch;  // [n] channel logits in global memory
 };
 
-// Element j + M 2^s of the stage-(s+T) node on the path to the channel, for the stage-s node at
-// pos (D = S - s stages below the channel).  c[m] = channel element j + m 2^s; base[t] =
-// start of the stage-(s+t+1) node + j (g at level t reads bit base[t] + M 2^s of the path).
-template <int D, int T, int M, int FM>
-__device__ __forceinline__ double vtree(const double* c, const uint32_t* bp, const int* base, uint32_t gmask, int hs,
+struct St {
+    unsigned char* smem;
+    Lay y;
+    const float* llr;
+    int64_t b0, bs;
+    int n, S, W, SS, per;
+    double lmax;
+    __device__ __forceinline__ Cw cw(int c) const {
+        unsigned char* base = smem + c * y.bytes;
+        Cw w;
+        w.A = reinterpret_cast<double*>(base + y.off_A);
+        w.beta = reinterpret_cast<uint32_t*>(base + y.off_beta);
+        w.sptr = base + y.off_sptr;
+        w.org_s = reinterpret_cast<int*>(base + y.off_org);
+        w.ps_s = reinterpret_cast<uint32_t*>(base + y.off_ps);
+        w.pm_s = reinterpret_cast<double*>(base + y.off_pm);
+        w.fail_s = reinterpret_cast<int*>(base + y.off_fail);
+        w.sv = reinterpret_cast<double*>(base + y.off_sv);
+        w.sp = reinterpret_cast<int*>(base + y.off_sp);
+        int64_t row = b0 + c;
+        if (row >= bs) row = bs - 1;  // a tail wave's missing codewords decode a copy, never stored
+        w.ch = llr + row * n;
+        return w;
+    }
+};
+
+// Input element j of the stage-s node at pos, V levels below the channel, bottom-up in place:
+// c[m] = negated channel element j + m 2^s (m < 2^V); level t (from the channel down) combines
+// v[m] and v[m + 2^t] (m < 2^t) with f, or with g reading bit base[t] + m 2^s of the path
+// (base[t] = start of the stage-(s+t+1) node + j) when the stage-(s+t) node is a right child.
+// The same f/g operands as the recursion over the tree, so the same values.
+template <int V, int FM>
+__device__ __forceinline__ double vtree(const float* c, const uint32_t* bp, const int* base, uint32_t gmask, int hs,
                                         double lmax) {
-    if constexpr (T == D) {
-        return c[M];
+    if constexpr (V == 0) {
+        return (double)c[0];
     } else {
-        const double x = vtree<D, T + 1, M, FM>(c, bp, base, gmask, hs, lmax);
-        const double y = vtree<D, T + 1, M + (1 << T), FM>(c, bp, base, gmask, hs, lmax);
-        if ((gmask >> T) & 1u) return g_op(x, y, getbit(bp, base[T] + M * hs));
-        return f_op<FM>(x, y, lmax);
+        constexpr int H = 1 << (V - 1);
+        double v[H];
+        {
+            constexpr int t = V - 1;
+            const bool g = (gmask >> t) & 1u;
+#pragma unroll
+            for (int m = 0; m < H; ++m) {
+                const double x = (double)c[m], y = (double)c[m + H];
+                v[m] = g ? g_op(x, y, getbit(bp, base[t] + m * hs)) : f_op<FM>(x, y, lmax);
+            }
+        }
+#pragma unroll
+        for (int t = V - 2; t >= 0; --t) {
+            const int h = 1 << t;
+            const bool g = (gmask >> t) & 1u;
+#pragma unroll
+            for (int m = 0; m < h; ++m)
+                v[m] = g ? g_op(v[m], v[m + h], getbit(bp, base[t] + m * hs)) : f_op<FM>(v[m], v[m + h], lmax);
+        }
+        return v[0];
     }
 }
 
 // Upper-tree node at stage s (> R), position pos: f (or g) of its input into the stage-(s-1)
-// buffers of every path (s-1 <= SS), wave-parallel over (path, element).  When the input is
-// virtual (s = SS + 1, V stages below the channel) each lane keeps one element j and loops over
-// the paths, so the 2 x 2^V channel values it needs are read once, not once per path.
-template <int L, int V, int FM>
+// buffers of every path of every codeword (s-1 <= SS), wave-parallel over (codeword, path,
+// element).  When the input is virtual (s = SS + 1, V stages below the channel) each lane keeps
+// one (codeword, element) and loops over the paths, so the 2 x 2^V channel values it needs are
+// read once, not once per path (lanes idle when the node has fewer than 64 / CPW elements).
+template <int L, int V, int FM, int CPW>
 __device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane) {
+    constexpr int LL = ilog2(L);
     const int ls = s - 1, h = 1 << ls;
-    if (s <= t.SS || h < 64) {
-        const int total = L * h;
+    if (s <= t.SS) {
+        const int total = CPW * L * h;
         for (int idx = lane; idx < total; idx += 64) {
-            const int p = idx >> ls, j = idx & (h - 1);
-            const uint32_t* bp = t.beta + p * t.W;
-            double x, y;
-            if (s <= t.SS) {
-                const double* in = t.A + t.sptr[p * (t.S + 1) + s] * t.per + (1 << s) - (1 << R);
-                x = in[j];
-                y = in[j + h];
-            } else {  // s == SS + 1: V stages below the channel
-                x = vread<V, FM>(t.ch, bp, s, pos, j, t.lmax);
-                y = vread<V, FM>(t.ch, bp, s, pos, j + h, t.lmax);
-            }
+            const int c = idx >> (LL + ls), p = (idx >> ls) & (L - 1), j = idx & (h - 1);
+            const Cw w = t.cw(c);
+            const uint32_t* bp = w.beta + p * t.W;
+            const double* in = w.A + w.sptr[p * (t.S + 1) + s] * t.per + (1 << s) - (1 << R);
+            const double x = in[j], y = in[j + h];
             const double r = is_g ? g_op(x, y, getbit(bp, pos + j)) : f_op<FM>(x, y, t.lmax);
-            t.A[p * t.per + (1 << ls) - (1 << R) + j] = r;
+            w.A[p * t.per + (1 << ls) - (1 << R) + j] = r;
         }
     } else {
         constexpr int NC = 1 << V;
@@ -190,12 +258,18 @@ __device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane) {
             bx[q] = pp;
             by[q] = pp + h;
         }
-        for (int j = lane; j < h; j += 64) {
-            double cx[NC], cy[NC];
+        // channel rows addressed from the wave's first row (uniform base, 32-bit lane offsets)
+        const float* ch0 = t.llr + t.b0 * t.n;
+#pragma unroll 1
+        for (int idx = lane; idx < CPW * h; idx += 64) {
+            const int c = idx >> ls, j = idx & (h - 1);
+            const Cw w = t.cw(c);
+            const int co = (int)(t.b0 + c < t.bs ? c : t.bs - 1 - t.b0) * t.n + j;
+            float cx[NC], cy[NC];
 #pragma unroll
             for (int m = 0; m < NC; ++m) {
-                cx[m] = (double)t.ch[j + m * hs];
-                cy[m] = (double)t.ch[j + h + m * hs];
+                cx[m] = -1.0f * ch0[co + m * hs];
+                cy[m] = -1.0f * ch0[co + h + m * hs];
             }
             int basex[V > 0 ? V : 1], basey[V > 0 ? V : 1];
 #pragma unroll
@@ -203,33 +277,44 @@ __device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane) {
                 basex[q] = bx[q] + j;
                 basey[q] = by[q] + j;
             }
+#pragma unroll 1
             for (int p = 0; p < L; ++p) {
-                const uint32_t* bp = t.beta + p * t.W;
-                const double x = vtree<V, 0, 0, FM>(cx, bp, basex, gmask, hs, t.lmax);
-                const double y = vtree<V, 0, 0, FM>(cy, bp, basey, gmask, hs, t.lmax);
+                const uint32_t* bp = w.beta + p * t.W;
+                // opaque per-iteration copies: the 2 (2^V - 1) bit addresses are recomputed per
+                // path instead of being hoisted out of the loop (register pressure, occupancy)
+                int bxp[V > 0 ? V : 1], byp[V > 0 ? V : 1];
+#pragma unroll
+                for (int q = 0; q < V; ++q) {
+                    bxp[q] = basex[q];
+                    byp[q] = basey[q];
+                    asm volatile("" : "+v"(bxp[q]), "+v"(byp[q]));
+                }
+                const double x = vtree<V, FM>(cx, bp, bxp, gmask, hs, t.lmax);
+                const double y = vtree<V, FM>(cy, bp, byp, gmask, hs, t.lmax);
                 const double r = is_g ? g_op(x, y, getbit(bp, pos + j)) : f_op<FM>(x, y, t.lmax);
-                t.A[p * t.per + (1 << ls) - (1 << R) + j] = r;
+                w.A[p * t.per + (1 << ls) - (1 << R) + j] = r;
             }
         }
     }
-    if (lane < L) t.sptr[lane * (t.S + 1) + ls] = (uint8_t)lane;
+    if (lane < CPW * L) t.cw(lane >> LL).sptr[(lane & (L - 1)) * (t.S + 1) + ls] = (uint8_t)(lane & (L - 1));
     __syncthreads();
 }
 
-// beta[pos, pos+h) ^= beta[pos+h, pos+2h) for every path, h = 2^(s-1): word XORs for h >= 32,
-// in-word bit ops below.
-template <int L>
+// beta[pos, pos+h) ^= beta[pos+h, pos+2h) for every path of every codeword, h = 2^(s-1): word
+// XORs for h >= 32, in-word bit ops below.
+template <int L, int CPW>
 __device__ void combine_upper(const St& t, int s, int pos, int lane) {
+    constexpr int LL = ilog2(L);
     const int h = 1 << (s - 1);
     if (h >= 32) {
-        const int hw = h >> 5, w0 = pos >> 5;
-        for (int idx = lane; idx < L * hw; idx += 64) {
-            const int p = idx / hw, w = idx - p * hw;
-            uint32_t* b = t.beta + p * t.W;
+        const int lhw = s - 6, hw = 1 << lhw, w0 = pos >> 5;
+        for (int idx = lane; idx < CPW * L * hw; idx += 64) {
+            const int c = idx >> (LL + lhw), p = (idx >> lhw) & (L - 1), w = idx & (hw - 1);
+            uint32_t* b = t.cw(c).beta + p * t.W;
             b[w0 + w] ^= b[w0 + hw + w];
         }
-    } else if (lane < L) {
-        uint32_t* b = t.beta + lane * t.W + (pos >> 5);
+    } else if (lane < CPW * L) {
+        uint32_t* b = t.cw(lane >> LL).beta + (lane & (L - 1)) * t.W + (pos >> 5);
         *b ^= (*b >> h) & (((1u << h) - 1u) << (pos & 31));
     }
     __syncthreads();
@@ -249,9 +334,6 @@ __device__ __forceinline__ void f_down(double* st, double lmax) {
     }
 }
 
-// stage-R input element j of a lane's subtree (the origin's stored buffer, or the channel)
-__device__ __forceinline__ double in_R(const St&, const double* inA, int j) { return inA[j]; }
-
 __device__ __forceinline__ void load_group_fence(int j) {
 #if PL_SCL_LOADGRP > 0
     if ((j + 1) % PL_SCL_LOADGRP == 0) __builtin_amdgcn_sched_barrier(0);
@@ -262,15 +344,15 @@ __device__ __forceinline__ void load_group_fence(int j) {
 
 // Leaf i (> 0) with tz = ctz(i) trailing zeros: g at stage tz+1 into stage tz, then f down.
 template <int tz, int FM>
-__device__ __forceinline__ void g_step(const St& t, const double* inA, double* st, uint32_t ps, int i) {
+__device__ __forceinline__ void g_step(const double* inA, double* st, uint32_t ps, int i, double lmax) {
     constexpr int h = 1 << tz;
     const int p0 = i - h;  // start of the left sibling, whose partial sums g consumes
 #pragma unroll
     for (int j = 0; j < h; ++j) {
         double x, y;
         if constexpr (tz + 1 == R) {
-            x = in_R(t, inA, j);
-            y = in_R(t, inA, j + h);
+            x = inA[j];
+            y = inA[j + h];
         } else {
             x = st[IDX(tz + 1) + j];
             y = st[IDX(tz + 1) + j + h];
@@ -278,27 +360,27 @@ __device__ __forceinline__ void g_step(const St& t, const double* inA, double* s
         st[IDX(tz) + j] = g_op(x, y, (ps >> (p0 + j)) & 1u);
         if constexpr (tz + 1 == R) load_group_fence(j);
     }
-    f_down<tz, FM>(st, t.lmax);
+    f_down<tz, FM>(st, lmax);
 }
 
 template <int FM>
-__device__ __forceinline__ void leaf_llr(const St& t, const double* inA, double* st, uint32_t ps, int i) {
+__device__ __forceinline__ void leaf_llr(const double* inA, double* st, uint32_t ps, int i, double lmax) {
     if (i == 0) {
         constexpr int h = T / 2;
 #pragma unroll
         for (int j = 0; j < h; ++j) {
-            st[IDX(R - 1) + j] = f_op<FM>(in_R(t, inA, j), in_R(t, inA, j + h), t.lmax);
+            st[IDX(R - 1) + j] = f_op<FM>(inA[j], inA[j + h], lmax);
             load_group_fence(j);
         }
-        f_down<R - 1, FM>(st, t.lmax);
+        f_down<R - 1, FM>(st, lmax);
         return;
     }
     switch (__builtin_ctz(i)) {
-        case 0: g_step<0, FM>(t, inA, st, ps, i); break;
-        case 1: g_step<1, FM>(t, inA, st, ps, i); break;
-        case 2: g_step<2, FM>(t, inA, st, ps, i); break;
-        case 3: g_step<3, FM>(t, inA, st, ps, i); break;
-        default: g_step<R - 1, FM>(t, inA, st, ps, i); break;
+        case 0: g_step<0, FM>(inA, st, ps, i, lmax); break;
+        case 1: g_step<1, FM>(inA, st, ps, i, lmax); break;
+        case 2: g_step<2, FM>(inA, st, ps, i, lmax); break;
+        case 3: g_step<3, FM>(inA, st, ps, i, lmax); break;
+        default: g_step<R - 1, FM>(inA, st, ps, i, lmax); break;
     }
 }
 
@@ -314,14 +396,18 @@ __device__ __forceinline__ void pull_live(double* st, int i, int src) {
     }
 }
 
-// Decode the stage-R node at absolute position i0 for every path (lanes < L own paths; the
-// other lanes shadow lane % L and are ignored).  pm, org: the lane's metric and origin.
-template <int L, int FM>
+// Decode the stage-R node at absolute position i0 for every path of every codeword of the wave
+// (group lanes < L own paths; group lanes >= L shadow lane gl - L).  pm, org: the lane's metric
+// and origin (path index inside the group).
+template <int L, int FM, int CPW>
 __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, uint32_t& ps, int lane) {
+    constexpr int GW = 2 * L;
+    const int gl = lane & (GW - 1), gbase = lane & ~(GW - 1);
+    const Cw w = t.cw(lane / GW);
     double st[T - 1];
     ps = 0u;
-    org = lane & (L - 1);
-    const double* inA = t.A + org * t.per;  // stage R sits at offset 0 of a path's region
+    org = gl & (L - 1);
+    const double* inA = w.A + org * t.per;  // stage R sits at offset 0 of a path's region
     for (int i = 0; i < T; ++i) {
         if (i > 0) {  // nodes that ended at leaf i-1 (stages 1..ctz(i)): [uL ^ uR, uR] (:147-153)
             const int tz = __builtin_ctz(i);
@@ -329,40 +415,44 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
                 const int h = 1 << (s - 1), pos = i - (1 << s);
                 ps ^= (ps >> h) & (((1u << h) - 1u) << pos);
             }
-            if (tz + 1 == R) inA = t.A + org * t.per;  // the origin may have changed
+            if (tz + 1 == R) inA = w.A + org * t.per;  // the origin may have changed
         }
-        leaf_llr<FM>(t, inA, st, ps, i);
+        leaf_llr<FM>(inA, st, ps, i, t.lmax);
         const double l = fmax(fmin(st[0], t.lmax), -t.lmax);
-        // metric update (:83): pen = log(1 + exp(-(1-2u) l)).  At an information leaf lanes
-        // c >= L (shadows of state c & (L-1)) evaluate u = 1, lanes c < L u = 0: one exp/log per
-        // lane gives all 2L candidates.  Same expression as the reference, so same rounding.
+        // metric update (:83): pen = log(1 + exp(-(1-2u) l)).  At an information leaf shadow
+        // lanes evaluate u = 1, path lanes u = 0: one exp/log per lane gives all 2L candidates.
+        // Same expression as the reference, so same rounding.
         const bool info = ((fz >> i) & 1u) == 0u;
-        const bool hi = (lane & L) != 0;
+        const bool hi = (gl & L) != 0;
         const double sl = (info && hi) ? -1.0 * l : 1.0 * l;
         const double pen = log(1.0 + exp(-sl));
         if (!info) {  // frozen leaf: metric update only (u = 0)
             pm = pm + pen;
             continue;
         }
-        // Lane c < 2L holds candidate c: c < L = (state c, u=0), c >= L = (state c-L, u=1).  Its
-        // rank in the stable (metric, index) order comes from 2L readlane broadcasts; one
-        // ds_permute then sends every candidate to the lane of its rank (ranks are a permutation
-        // of [0, 2L); lanes >= 2L send to themselves, so every lane is written exactly once), and
-        // slots >= L re-shadow slot & (L-1).
+        // Group lane c holds candidate c: c < L = (state c, u=0), c >= L = (state c-L, u=1).  Its
+        // rank in the stable (metric, index) order comes from 2L-1 in-group broadcasts; one
+        // ds_permute then sends every candidate to the group lane of its rank (ranks are a
+        // permutation of [0, 2L), so every lane is written exactly once), and slots >= L
+        // re-shadow slot - L.
         const double cv = pm + pen;
         int rk = 0;
+        if constexpr (GW == 64) {
 #pragma unroll
-        for (int c = 0; c < 2 * L; ++c) {
-            const double v = readlane_d(cv, c);
-            rk += (v < cv || (v == cv && c < lane)) ? 1 : 0;
+            for (int c = 0; c < 2 * L; ++c) {
+                const double v = readlane_d(cv, c);
+                rk += (v < cv || (v == cv && c < lane)) ? 1 : 0;
+            }
+        } else {
+            rank_rot<GW, 1>(cv, gl, lane, rk);
         }
-        const int dst = lane < 2 * L ? rk : lane;
-        const int code = (lane & (L - 1)) | (hi ? 256 : 0);
+        const int dst = gbase + rk;
+        const int code = (gl & (L - 1)) | (hi ? 256 : 0);
         const long long cb = __double_as_longlong(cv);
         int rcode = __builtin_amdgcn_ds_permute(dst << 2, code);
         int rlo = __builtin_amdgcn_ds_permute(dst << 2, (int)(cb & 0xffffffffLL));
         int rhi = __builtin_amdgcn_ds_permute(dst << 2, (int)(cb >> 32));
-        const int me = lane & (L - 1);
+        const int me = gbase + (gl & (L - 1));
         rcode = bperm_i(rcode, me);
         rlo = bperm_i(rlo, me);
         rhi = bperm_i(rhi, me);
@@ -370,10 +460,10 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
         const uint32_t bit = (uint32_t)rcode >> 8;
         const double npm = __longlong_as_double(((long long)rhi << 32) | (unsigned int)rlo);
         pm = npm;
-        ps = (uint32_t)bperm_i((int)ps, par) | (bit << i);
-        org = bperm_i(org, par);
-        inA = t.A + org * t.per;
-        pull_live<R - 1>(st, i, par);
+        ps = (uint32_t)bperm_i((int)ps, gbase + par) | (bit << i);
+        org = bperm_i(org, gbase + par);
+        inA = w.A + org * t.per;
+        pull_live<R - 1>(st, i, gbase + par);
     }
     for (int s = 1; s <= R; ++s) {  // the nodes ending at the last leaf, up to stage R
         const int h = 1 << (s - 1), pos = T - (1 << s);
@@ -391,41 +481,38 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
                                                       const uint32_t* __restrict__ frozen_words,
                                                       const int32_t* __restrict__ info_pos, int n, int S, int k,
                                                       double lmax, int crc_deg, uint32_t crc_g) {
+    constexpr int GW = 2 * L, CPW = 64 / GW, LL = ilog2(L);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const Lay y = make_layout(n, S, L, V);
     const int lane = threadIdx.x;
-    const int64_t b = blockIdx.x;
     St t;
-    t.A = reinterpret_cast<double*>(smem + y.off_A);
-    t.ch = reinterpret_cast<float*>(smem + y.off_ch);
-    t.beta = reinterpret_cast<uint32_t*>(smem + y.off_beta);
-    t.sptr = smem + y.off_sptr;
-    t.org_s = reinterpret_cast<int*>(smem + y.off_org);
-    t.ps_s = reinterpret_cast<uint32_t*>(smem + y.off_ps);
+    t.smem = smem;
+    t.y = make_layout(n, S, L, V);
+    t.llr = llr;
+    t.b0 = (int64_t)blockIdx.x * CPW;
+    t.bs = bs;
     t.n = n;
     t.S = S;
-    t.W = y.W;
-    t.SS = y.SS;
-    t.per = y.per;
+    t.W = t.y.W;
+    t.SS = t.y.SS;
+    t.per = t.y.per;
     t.lmax = lmax;
-    double* pm_s = reinterpret_cast<double*>(smem + y.off_pm);
-    int* fail_s = reinterpret_cast<int*>(smem + y.off_fail);
+    const int W = t.W, LW = ilog2(W);
+    const int gl = lane & (GW - 1), my_c = lane / GW;
+    const Cw mine = t.cw(my_c);
 
-    {
-        const float4* x4 = reinterpret_cast<const float4*>(llr + b * n);
-        float4* c4 = reinterpret_cast<float4*>(t.ch);
-        for (int i = lane; i < n / 4; i += 64) {
-            const float4 v = x4[i];
-            c4[i] = make_float4(-1.0f * v.x, -1.0f * v.y, -1.0f * v.z, -1.0f * v.w);  // polar_scl.py:219
-        }
+    for (int i = lane; i < CPW * L * W; i += 64) t.cw(i >> (LL + LW)).beta[i & (L * W - 1)] = 0u;
+    for (int i = lane; i < CPW * L * (S + 1); i += 64) {
+        const int c = i / (L * (S + 1)), e = i - c * (L * (S + 1));
+        t.cw(c).sptr[e] = (uint8_t)(e / (S + 1));
     }
-    for (int i = lane; i < L * y.W; i += 64) t.beta[i] = 0u;
-    for (int i = lane; i < L * (S + 1); i += 64) t.sptr[i] = (uint8_t)(i / (S + 1));
     if (S == R)  // the whole tree is one lane-local subtree: its input is the channel, as fp64
-        for (int i = lane; i < T; i += 64) t.A[i] = (double)t.ch[i];
+        for (int i = lane; i < CPW * T; i += 64) {
+            const Cw w = t.cw(i / T);
+            w.A[i % T] = (double)(-1.0f * w.ch[i % T]);
+        }
     __syncthreads();
 
-    double pm = (lane & (L - 1)) == 0 ? 0.0 : lmax;  // :192-194 ([0, 30 x (L-1)] per half)
+    double pm = gl == 0 || gl == L ? 0.0 : lmax;  // :192-194 ([0, 30 x (L-1)] per half)
     const int nsub = n >> R;
     for (int q = 0; q < nsub; ++q) {
         const int i0 = q << R;
@@ -433,88 +520,103 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
         // then f down to stage R (stored stages only; virtual ones are recomputed on read)
         if (q == 0) {
             for (int s = S; s > R; --s)
-                if (s - 1 <= t.SS) node_fg<L, V, FM>(t, s, 0, false, lane);
+                if (s - 1 <= t.SS) node_fg<L, V, FM, CPW>(t, s, 0, false, lane);
         } else {
             const int tz = __builtin_ctz(i0);
-            if (tz <= t.SS) node_fg<L, V, FM>(t, tz + 1, i0 & ~((2 << tz) - 1), true, lane);
+            if (tz <= t.SS) node_fg<L, V, FM, CPW>(t, tz + 1, i0 & ~((2 << tz) - 1), true, lane);
             for (int s = tz; s > R; --s)
-                if (s - 1 <= t.SS) node_fg<L, V, FM>(t, s, i0, false, lane);
+                if (s - 1 <= t.SS) node_fg<L, V, FM, CPW>(t, s, i0, false, lane);
         }
         int org;
         uint32_t ps;
-        subtree<L, FM>(t, i0, frozen_words[i0 >> 5] >> (i0 & 31), pm, org, ps, lane);
+        subtree<L, FM, CPW>(t, i0, frozen_words[i0 >> 5] >> (i0 & 31), pm, org, ps, lane);
         // re-point the upper-tree state of every path to its origin's, then store the
         // subtree's partial sums: partial-sum words before i0 and stage owners R..SS
-        if (lane < L) {
-            t.org_s[lane] = org;
-            t.ps_s[lane] = ps;
+        if (gl < L) {
+            mine.org_s[gl] = org;
+            mine.ps_s[gl] = ps;
         }
         __syncthreads();
         const int w_i = i0 >> 5, w_lim = (i0 + 31) >> 5, off = i0 & 31;
-        constexpr int RB = (L * 32 + 63) / 64;  // <= L*W/64 words per lane (n <= 1024)
+        // CPW * L = 32 (codeword, path) pairs per wave, <= 32 words each (n <= 1024)
+        constexpr int RB = 32 * 32 / 64;
         uint32_t vb[RB];
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
             const int idx = r * 64 + lane;
-            const int np = idx >> 5, w = idx & 31;
-            if (np < L && w < w_lim) vb[r] = t.beta[t.org_s[np] * y.W + w];
+            const int cp = idx >> 5, w = idx & 31;
+            if (w < w_lim) {
+                const Cw cw = t.cw(cp >> LL);
+                vb[r] = cw.beta[cw.org_s[cp & (L - 1)] * W + w];
+            }
         }
-        constexpr int RS = (L * 11 + 63) / 64;
+        constexpr int RS = (32 * 11 + 63) / 64;
         uint8_t vs[RS];
         const int S1 = S + 1;
 #pragma unroll
         for (int r = 0; r < RS; ++r) {
             const int idx = r * 64 + lane;
-            if (idx < L * S1) vs[r] = t.sptr[t.org_s[idx / S1] * S1 + idx % S1];
+            if (idx < 32 * S1) {
+                const int cp = idx / S1, e = idx - cp * S1;
+                const Cw cw = t.cw(cp >> LL);
+                vs[r] = cw.sptr[cw.org_s[cp & (L - 1)] * S1 + e];
+            }
         }
         __syncthreads();
 #pragma unroll
         for (int r = 0; r < RB; ++r) {
             const int idx = r * 64 + lane;
-            const int np = idx >> 5, w = idx & 31;
-            if (np < L && w < w_lim) t.beta[np * y.W + w] = vb[r];
+            const int cp = idx >> 5, w = idx & 31;
+            if (w < w_lim) t.cw(cp >> LL).beta[(cp & (L - 1)) * W + w] = vb[r];
         }
 #pragma unroll
         for (int r = 0; r < RS; ++r) {
             const int idx = r * 64 + lane;
-            if (idx < L * S1) t.sptr[idx] = vs[r];
+            if (idx < 32 * S1) {
+                const int cp = idx / S1, e = idx - cp * S1;
+                t.cw(cp >> LL).sptr[(cp & (L - 1)) * S1 + e] = vs[r];
+            }
         }
         if (T < 32 && off != 0) __syncthreads();  // the word's low part was just copied
-        if (lane < L) {
-            uint32_t* bw = t.beta + lane * y.W + w_i;
+        if (gl < L) {
+            uint32_t* bw = mine.beta + gl * W + w_i;
             *bw = off == 0 ? ps : ((*bw & ((1u << off) - 1u)) | (ps << off));
         }
         __syncthreads();
         // nodes above R that end with this subtree
         const int nxt = i0 + T;
         const int top = nxt < n ? __builtin_ctz(nxt) : S;
-        for (int s = R + 1; s <= top; ++s) combine_upper<L>(t, s, nxt - (1 << s), lane);
+        for (int s = R + 1; s <= top; ++s) combine_upper<L, CPW>(t, s, nxt - (1 << s), lane);
     }
-    if (lane < L) pm_s[lane] = pm;
+    if (gl < L) mine.pm_s[gl] = pm;
 
     // u = x G_n per path (x = the root's partial sums): in-word spans, then word spans
-    for (int idx = lane; idx < L * y.W; idx += 64) {
-        uint32_t w = t.beta[idx];
+    for (int idx = lane; idx < CPW * L * W; idx += 64) {
+        uint32_t* bw = t.cw(idx >> (LL + LW)).beta + (idx & (L * W - 1));
+        uint32_t w = *bw;
         w ^= (w >> 1) & 0x55555555u;
         w ^= (w >> 2) & 0x33333333u;
         w ^= (w >> 4) & 0x0f0f0f0fu;
         w ^= (w >> 8) & 0x00ff00ffu;
         w ^= (w >> 16) & 0x0000ffffu;
-        t.beta[idx] = w;
+        *bw = w;
     }
     __syncthreads();
-    for (int m = 1; m < y.W; m <<= 1) {
-        for (int idx = lane; idx < L * y.W; idx += 64)
-            if ((idx & m) == 0) t.beta[idx] ^= t.beta[idx + m];
+    for (int m = 1; m < W; m <<= 1) {
+        for (int idx = lane; idx < CPW * L * W; idx += 64) {
+            if ((idx & m) == 0) {
+                uint32_t* bw = t.cw(idx >> (LL + LW)).beta + (idx & (L * W - 1));
+                bw[0] ^= bw[m];
+            }
+        }
         __syncthreads();
     }
 
-    // CRC check per path (my_sn dec.py:507-518), final stable sort of the 2L logical rows
-    // (row r < L = state r, row r >= L its copy), penalty per failing row, first argmin (:224)
-    if (lane < L) {
+    // CRC check per path (my_sn dec.py:507-518)
+    if (gl < L) {
         int f = 0;
         if (crc_deg > 0) {
-            const uint32_t* U = t.beta + lane * y.W;
+            const uint32_t* U = mine.beta + gl * W;
             const uint32_t mask = (1u << crc_deg) - 1u;
             uint32_t reg = 0;
             for (int m = 0; m < k; ++m) {
@@ -525,39 +627,48 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
             }
             f = reg != 0u;
         }
-        fail_s[lane] = f;
+        mine.fail_s[gl] = f;
     }
     __syncthreads();
-    int best = 0;
+    // Final stable sort of the 2L logical rows (row r < L = state r, row r >= L its copy) by
+    // metric, penalty per failing row, first argmin in that order (:204-206, :224): group lane
+    // r ranks row r and files it at its rank; the group's first lane scans the sorted rows.
     {
-        int row[64];
-        for (int r = 0; r < 2 * L; ++r) row[r] = r;
-        for (int a = 1; a < 2 * L; ++a) {
-            const int v = row[a];
-            int c = a - 1;
-            while (c >= 0 && pm_s[row[c] % L] > pm_s[v % L]) {
-                row[c + 1] = row[c];
-                --c;
-            }
-            row[c + 1] = v;
+        const int p = gl & (L - 1);
+        const double mv = mine.pm_s[p];
+        int rk = 0;
+        for (int c = 0; c < GW; ++c) {
+            const double v = mine.pm_s[c & (L - 1)];
+            rk += (v < mv || (v == mv && c < gl)) ? 1 : 0;
         }
-        double bestv = 0.0;
-        for (int r = 0; r < 2 * L; ++r) {
-            const int p = row[r] % L;
-            const double v = pm_s[p] + (fail_s[p] ? 30.0 * (double)k : 0.0);
-            if (out_pm != nullptr && lane == 0) out_pm[b * 2 * L + r] = v;
-            if (r == 0 || v < bestv) {
-                best = p;
-                bestv = v;
-            }
-        }
+        const double val = mv + (mine.fail_s[p] ? 30.0 * (double)k : 0.0);
+        mine.sv[rk] = val;
+        mine.sp[rk] = p;
+        if (out_pm != nullptr && t.b0 + my_c < bs) out_pm[(t.b0 + my_c) * GW + rk] = val;
     }
-    const uint32_t* U = t.beta + best * y.W;
-    for (int m = lane; m < k; m += 64) {
-        const int pos = info_pos[m];
-        const uint32_t bit = (U[pos >> 5] >> (pos & 31)) & 1u;
-        if (out_kind == PL_OUT_F32) static_cast<float*>(out)[b * k + m] = bit ? 1.0f : 0.0f;
-        else static_cast<uint8_t*>(out)[b * k + m] = (uint8_t)bit;
+    __syncthreads();
+    if (gl == 0) {
+        double bestv = mine.sv[0];
+        int best = mine.sp[0];
+        for (int r = 1; r < GW; ++r)
+            if (mine.sv[r] < bestv) {
+                bestv = mine.sv[r];
+                best = mine.sp[r];
+            }
+        mine.org_s[0] = best;
+    }
+    __syncthreads();
+    for (int c = 0; c < CPW; ++c) {
+        const int64_t b = t.b0 + c;
+        if (b >= bs) break;
+        const Cw w = t.cw(c);
+        const uint32_t* U = w.beta + w.org_s[0] * W;
+        for (int m = lane; m < k; m += 64) {
+            const int pos = info_pos[m];
+            const uint32_t bit = (U[pos >> 5] >> (pos & 31)) & 1u;
+            if (out_kind == PL_OUT_F32) static_cast<float*>(out)[b * k + m] = bit ? 1.0f : 0.0f;
+            else static_cast<uint8_t*>(out)[b * k + m] = (uint8_t)bit;
+        }
     }
 }
 
@@ -591,8 +702,9 @@ const void* scl_tree_fn<PL_SCL_TREE_L>(int v, bool exact) {
 #ifdef PL_SCL_TREE_DISPATCH
 namespace {
 int pick_v(int S) {
-    int vmax = 3;
+    int vmax = 4;  // the channel is read from global memory, so virtual stages cost no LDS
     if (const char* e = getenv("PL_SCL_VIRTUAL")) vmax = atoi(e);
+    if (vmax > 4) vmax = 4;  // instantiated: V = 0..4 (the kernel's layout must match the host's)
     int v = S - 1 - R;
     if (v > vmax) v = vmax;
     return v < 0 ? 0 : v;
@@ -635,8 +747,10 @@ int launch_scl_tree(const pl_plan* p, const float* llr, int64_t bs, void* out, i
     }
 #endif
     const Lay y = make_layout(p->n, S, L, V);
-    if (y.bytes > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, y.bytes);
+    const int cpw = 32 / L;  // codewords per wave (one 2L-lane group each)
+    const int lds = cpw * y.bytes;
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return check_hip(e, "SCL decode: LDS attribute");
     }
     int n = p->n, k = p->k, cdeg = p->crc_deg;
@@ -646,7 +760,8 @@ int launch_scl_tree(const pl_plan* p, const float* llr, int64_t bs, void* out, i
     const int32_t* ip = p->d_info_pos;
     void* args[] = {(void*)&llr, (void*)&bs, (void*)&out, (void*)&out_kind, (void*)&out_pm, (void*)&fw,
                     (void*)&ip, (void*)&n, (void*)&S, (void*)&k, (void*)&lmax, (void*)&cdeg, (void*)&cg};
-    hipError_t e = hipLaunchKernel(fn, dim3((unsigned)bs), dim3(64), args, y.bytes, st);
+    const int64_t blocks = (bs + cpw - 1) / cpw;
+    hipError_t e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(64), args, lds, st);
     if (e != hipSuccess) return check_hip(e, "SCL decode launch (subtree kernel)");
     return check_hip(hipGetLastError(), "SCL decode launch (subtree kernel)");
 }
