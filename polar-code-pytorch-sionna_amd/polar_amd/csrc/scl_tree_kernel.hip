@@ -425,7 +425,11 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
         const bool info = ((fz >> i) & 1u) == 0u;
         const bool hi = (gl & L) != 0;
         const double sl = (info && hi) ? -1.0 * l : 1.0 * l;
+#if PL_SCL_DIAG_CHEAP_PEN  // timing diagnostic only (wrong metrics)
+        const double pen = fmax(-sl, 0.0);
+#else
         const double pen = log(1.0 + exp(-sl));
+#endif
         if (!info) {  // frozen leaf: metric update only (u = 0)
             pm = pm + pen;
             continue;
@@ -437,6 +441,11 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
         // re-shadow slot - L.
         const double cv = pm + pen;
         int rk = 0;
+#if PL_SCL_DIAG_NO_RANK  // timing diagnostic only (wrong selection)
+        if (true) {
+            rk = gl;
+        } else
+#endif
         if constexpr (GW == 64) {
 #pragma unroll
             for (int c = 0; c < 2 * L; ++c) {
