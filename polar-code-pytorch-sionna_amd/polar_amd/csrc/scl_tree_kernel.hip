@@ -48,6 +48,18 @@ namespace {
 #ifndef PL_SCL_LOADGRP
 #define PL_SCL_LOADGRP 0  // > 0: stage-R input read in groups of this many pairs (caps VGPRs)
 #endif
+#ifndef PL_SCL_UNROLL
+#define PL_SCL_UNROLL 1  // 1: the 2^R leaves of a lane-local subtree fully unrolled (A/B: 2.08 vs 2.27 ms)
+#endif
+#ifndef PL_SCL_DIAG_NO_UPPER
+#define PL_SCL_DIAG_NO_UPPER 0
+#endif
+#ifndef PL_SCL_DIAG_SKIP_V
+#define PL_SCL_DIAG_SKIP_V 0
+#endif
+#ifndef PL_SCL_DIAG_SKIP_ST
+#define PL_SCL_DIAG_SKIP_ST 0
+#endif
 #ifndef PL_SCL_WPE
 #define PL_SCL_WPE 2  // > 0: amdgpu_waves_per_eu minimum (2: <= 256 VGPRs, A/B on MI355X: 2.30 vs 3.62 ms at V=4)
 #endif
@@ -226,6 +238,127 @@ __device__ __forceinline__ double vtree(const float* c, const uint32_t* bp, cons
     }
 }
 
+// Virtual node of 64 (n = 1024, V = 4, h = 32): the input pair (x, y) = elements (j, j + 32) of
+// the stage-6 node at pos, rebuilt bottom-up from the channel.  Level q (stage 6 + q) combines
+// v[m] and v[m + 2^q], m < 2^q: f when the stage-(6+q) node is a left child, else g with bit j
+// of partial-sum word wb[q] + 2m (x) or the next word (y) -- one 16-byte load brings the words
+// of leaves m and m+1 for x and y.  The leading f levels (from the channel down to the first g)
+// do not depend on the path: they are computed once per element, the rest once per path.
+template <int q, int FM>
+__device__ __forceinline__ void vlev_f(double* vx, double* vy, double lmax) {
+    constexpr int h = 1 << q;
+#pragma unroll
+    for (int m = 0; m < h; ++m) {
+        vx[m] = f_op<FM>(vx[m], vx[m + h], lmax);
+        vy[m] = f_op<FM>(vy[m], vy[m + h], lmax);
+    }
+}
+template <int q>
+__device__ __forceinline__ void vlev_g(double* vx, double* vy, const uint32_t* wq, int j) {
+    constexpr int h = 1 << q;
+    if constexpr (h == 1) {
+        const uint2 u2 = *reinterpret_cast<const uint2*>(wq);
+        vx[0] = g_op(vx[0], vx[1], (u2.x >> j) & 1u);
+        vy[0] = g_op(vy[0], vy[1], (u2.y >> j) & 1u);
+    } else {
+#pragma unroll
+        for (int m = 0; m < h; m += 2) {
+            const uint4 u4 = *reinterpret_cast<const uint4*>(wq + 2 * m);
+            vx[m] = g_op(vx[m], vx[m + h], (u4.x >> j) & 1u);
+            vy[m] = g_op(vy[m], vy[m + h], (u4.y >> j) & 1u);
+            vx[m + 1] = g_op(vx[m + 1], vx[m + 1 + h], (u4.z >> j) & 1u);
+            vy[m + 1] = g_op(vy[m + 1], vy[m + 1 + h], (u4.w >> j) & 1u);
+        }
+    }
+}
+template <int Q, int FM>
+__device__ __forceinline__ void vlev_path(double* vx, double* vy, const uint32_t* bp, const int* wb, int j,
+                                          uint32_t gmask, double lmax) {
+    if constexpr (Q >= 0) {
+        if ((gmask >> Q) & 1u) vlev_g<Q>(vx, vy, bp + wb[Q], j);
+        else vlev_f<Q, FM>(vx, vy, lmax);
+        vlev_path<Q - 1, FM>(vx, vy, bp, wb, j, gmask, lmax);
+    }
+}
+template <int Q, int QE, int FM>  // shared f levels Q down to QE
+__device__ __forceinline__ void vlev_shared(double* vx, double* vy, double lmax) {
+    if constexpr (Q >= QE) {
+        vlev_f<Q, FM>(vx, vy, lmax);
+        vlev_shared<Q - 1, QE, FM>(vx, vy, lmax);
+    }
+}
+
+template <int L, int V, int NS, int FM>
+__device__ __forceinline__ void vnode64(const St& t, const Cw& w, const float* cx, const float* cy, const int* wb,
+                                        int j, uint32_t gmask, bool is_g, int pos, int ls) {
+    constexpr int H = 1 << (V - 1);       // values per side after the channel level
+    constexpr int K = NS > 0 ? (2 * H) >> NS : 2 * H;  // per side after the shared levels
+    double sx[K], sy[K];
+    if constexpr (NS > 0) {
+        double vx[H], vy[H];
+#pragma unroll
+        for (int m = 0; m < H; ++m) {
+            vx[m] = f_op<FM>((double)cx[m], (double)cx[m + H], t.lmax);
+            vy[m] = f_op<FM>((double)cy[m], (double)cy[m + H], t.lmax);
+        }
+        vlev_shared<V - 2, V - NS, FM>(vx, vy, t.lmax);
+#pragma unroll
+        for (int m = 0; m < K; ++m) {
+            sx[m] = vx[m];
+            sy[m] = vy[m];
+        }
+    }
+#pragma unroll 1
+    for (int p = 0; p < L; ++p) {
+        const uint32_t* bp = w.beta + p * t.W;
+        double vx[H], vy[H];
+        if constexpr (NS == 0) {  // the channel level is a g: per path
+            const uint32_t* wq = bp + wb[V - 1];
+#pragma unroll
+            for (int m = 0; m < H; m += 2) {
+                const uint4 u4 = *reinterpret_cast<const uint4*>(wq + 2 * m);
+                vx[m] = g_op((double)cx[m], (double)cx[m + H], (u4.x >> j) & 1u);
+                vy[m] = g_op((double)cy[m], (double)cy[m + H], (u4.y >> j) & 1u);
+                vx[m + 1] = g_op((double)cx[m + 1], (double)cx[m + 1 + H], (u4.z >> j) & 1u);
+                vy[m + 1] = g_op((double)cy[m + 1], (double)cy[m + 1 + H], (u4.w >> j) & 1u);
+            }
+            vlev_path<V - 2, FM>(vx, vy, bp, wb, j, gmask, t.lmax);
+        } else {
+#pragma unroll
+            for (int m = 0; m < K; ++m) {
+                vx[m] = sx[m];
+                vy[m] = sy[m];
+            }
+            vlev_path<V - NS - 1, FM>(vx, vy, bp, wb, j, gmask, t.lmax);
+        }
+        const double x = vx[0], y = vy[0];
+        const double r = is_g ? g_op(x, y, getbit(bp, pos + j)) : f_op<FM>(x, y, t.lmax);
+        w.A[p * t.per + (1 << ls) - (1 << R) + j] = r;
+    }
+}
+
+// One pass of a virtual node of 64 over the wave's (codeword, element) pairs; NS leading f
+// levels (a per-pass constant, so each NS is its own loop).
+template <int L, int V, int NS, int FM, int CPW>
+__device__ void vvisit64(const St& t, int pos, bool is_g, int lane, const int* wb, uint32_t gmask) {
+    constexpr int NC = 1 << V, ls = 5, h = 32, hs = 64;
+    // channel rows addressed from the wave's first row (uniform base, 32-bit lane offsets)
+    const float* ch0 = t.llr + t.b0 * t.n;
+#pragma unroll 1
+    for (int idx = lane; idx < CPW * h; idx += 64) {
+        const int c = idx >> ls, j = idx & (h - 1);
+        const Cw w = t.cw(c);
+        const int co = (int)(t.b0 + c < t.bs ? c : t.bs - 1 - t.b0) * t.n + j;
+        float cx[NC], cy[NC];
+#pragma unroll
+        for (int m = 0; m < NC; ++m) {
+            cx[m] = -1.0f * ch0[co + m * hs];
+            cy[m] = -1.0f * ch0[co + h + m * hs];
+        }
+        vnode64<L, V, NS, FM>(t, w, cx, cy, wb, j, gmask, is_g, pos, ls);
+    }
+}
+
 // Upper-tree node at stage s (> R), position pos: f (or g) of its input into the stage-(s-1)
 // buffers of every path of every codeword (s-1 <= SS), wave-parallel over (codeword, path,
 // element).  When the input is virtual (s = SS + 1, V stages below the channel) each lane keeps
@@ -235,7 +368,9 @@ template <int L, int V, int FM, int CPW>
 __device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane) {
     constexpr int LL = ilog2(L);
     const int ls = s - 1, h = 1 << ls;
-    if (s <= t.SS) {
+    if (PL_SCL_DIAG_SKIP_V && s > t.SS) {
+    } else if (PL_SCL_DIAG_SKIP_ST && s <= t.SS) {
+    } else if (s <= t.SS) {
         const int total = CPW * L * h;
         for (int idx = lane; idx < total; idx += 64) {
             const int c = idx >> (LL + ls), p = (idx >> ls) & (L - 1), j = idx & (h - 1);
@@ -258,6 +393,21 @@ __device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane) {
             bx[q] = pp;
             by[q] = pp + h;
         }
+        if constexpr (V == 4 && FM == 0) {  // pick_v: V = 4 only at n = 1024 (node of 64); exact f:
+            // the generic loop below (inlining 5 variants of the exp/log f spills heavily)
+            int wb[V];
+#pragma unroll
+            for (int q = 0; q < V; ++q) wb[q] = bx[q] >> 5;  // multiples of 4 words: aligned
+            // leading f levels from the channel down: path-independent
+            const int ns = (gmask & 8u) ? 0 : (gmask & 4u) ? 1 : (gmask & 2u) ? 2 : (gmask & 1u) ? 3 : 4;
+            switch (ns) {
+                case 0: vvisit64<L, V, 0, FM, CPW>(t, pos, is_g, lane, wb, gmask); break;
+                case 1: vvisit64<L, V, 1, FM, CPW>(t, pos, is_g, lane, wb, gmask); break;
+                case 2: vvisit64<L, V, 2, FM, CPW>(t, pos, is_g, lane, wb, gmask); break;
+                case 3: vvisit64<L, V, 3, FM, CPW>(t, pos, is_g, lane, wb, gmask); break;
+                default: vvisit64<L, V, 4, FM, CPW>(t, pos, is_g, lane, wb, gmask); break;
+            }
+        } else {
         // channel rows addressed from the wave's first row (uniform base, 32-bit lane offsets)
         const float* ch0 = t.llr + t.b0 * t.n;
 #pragma unroll 1
@@ -277,6 +427,7 @@ __device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane) {
                 basex[q] = bx[q] + j;
                 basey[q] = by[q] + j;
             }
+
 #pragma unroll 1
             for (int p = 0; p < L; ++p) {
                 const uint32_t* bp = w.beta + p * t.W;
@@ -294,6 +445,7 @@ __device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane) {
                 const double r = is_g ? g_op(x, y, getbit(bp, pos + j)) : f_op<FM>(x, y, t.lmax);
                 w.A[p * t.per + (1 << ls) - (1 << R) + j] = r;
             }
+        }
         }
     }
     if (lane < CPW * L) t.cw(lane >> LL).sptr[(lane & (L - 1)) * (t.S + 1) + ls] = (uint8_t)(lane & (L - 1));
@@ -408,6 +560,9 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
     ps = 0u;
     org = gl & (L - 1);
     const double* inA = w.A + org * t.per;  // stage R sits at offset 0 of a path's region
+#if PL_SCL_UNROLL
+#pragma unroll
+#endif
     for (int i = 0; i < T; ++i) {
         if (i > 0) {  // nodes that ended at leaf i-1 (stages 1..ctz(i)): [uL ^ uR, uR] (:147-153)
             const int tz = __builtin_ctz(i);
@@ -472,7 +627,9 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
         ps = (uint32_t)bperm_i((int)ps, gbase + par) | (bit << i);
         org = bperm_i(org, gbase + par);
         inA = w.A + org * t.per;
+#if !PL_SCL_DIAG_NO_PULL  // timing diagnostic only
         pull_live<R - 1>(st, i, gbase + par);
+#endif
     }
     for (int s = 1; s <= R; ++s) {  // the nodes ending at the last leaf, up to stage R
         const int h = 1 << (s - 1), pos = T - (1 << s);
@@ -527,10 +684,14 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
         const int i0 = q << R;
         // input of the stage-R node at i0: g of the node that ends the finished left sibling,
         // then f down to stage R (stored stages only; virtual ones are recomputed on read)
+#if PL_SCL_DIAG_NO_UPPER  // timing diagnostic only
+        if (q < 0) {
+#else
         if (q == 0) {
+#endif
             for (int s = S; s > R; --s)
                 if (s - 1 <= t.SS) node_fg<L, V, FM, CPW>(t, s, 0, false, lane);
-        } else {
+        } else if (!PL_SCL_DIAG_NO_UPPER) {
             const int tz = __builtin_ctz(i0);
             if (tz <= t.SS) node_fg<L, V, FM, CPW>(t, tz + 1, i0 & ~((2 << tz) - 1), true, lane);
             for (int s = tz; s > R; --s)
@@ -716,6 +877,7 @@ int pick_v(int S) {
     if (vmax > 4) vmax = 4;  // instantiated: V = 0..4 (the kernel's layout must match the host's)
     int v = S - 1 - R;
     if (v > vmax) v = vmax;
+    if (v == 4 && S != 10) v = 3;  // the V = 4 instance assumes n = 1024 (virtual node of 64)
     return v < 0 ? 0 : v;
 }
 }  // namespace

@@ -95,7 +95,7 @@ def test_scl_subtree_equals_generic(pa, log_n, L, f_mode):
     rng = np.random.default_rng(1000 * log_n + L + 7 * f_mode)
     for k in (n // 4, n // 2, n - 3):
         fp = np.sort(rng.permutation(n)[: n - k])
-        bs = 96
+        bs = 93  # ragged: not a multiple of the subtree kernel's codewords per wave (32 / L)
         llr = (rng.standard_normal((bs, n)) * 2.5 + 0.5).astype(np.float32)
         llr[:8] = np.round(llr[:8])
         llr[8:12] *= 40.0
