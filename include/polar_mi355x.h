@@ -63,7 +63,8 @@ typedef struct pl_plan pl_plan;
 /* Build an immutable decoding plan for a length-n polar code.
  * frozen_mask: HOST pointer to n bytes, nonzero = frozen position (frozen_pos of the reference).
  * list_size:   1 for SC plans; a power of two <= 32 for SCL plans.
- * f_mode:      PL_F_MINSUM or PL_F_EXACT.  llr_max: clipping bound (reference: 30).
+ * f_mode:      PL_F_MINSUM or PL_F_EXACT.  llr_max: clipping bound (reference: 30; at most 700
+ *              for list_size > 1, where log(1 + exp(llr_max)) must stay finite).
  * flags:       0, or PL_PLAN_GENERIC / PL_PLAN_CACHE_ONLY.  By default an SC plan (list_size 1)
  *              runs a kernel specialised to its frozen set: compiled with hiprtc at plan creation
  *              (seconds) unless a cached code object exists ($PL_KERNEL_CACHE, <library dir>/kcache,

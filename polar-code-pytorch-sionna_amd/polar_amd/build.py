@@ -57,7 +57,7 @@ def build(force=False, verbose=False):
     hipcc = _hipcc()
     os.makedirs(OBJ, exist_ok=True)
     inc = _embed_static_source()
-    deps = [os.path.join(CSRC, "plan.h"),
+    deps = [os.path.join(CSRC, "plan.h"), os.path.join(CSRC, "softplus.h"),
             os.path.join(HERE, "..", "..", "include", "polar_mi355x.h")]
     jobs = []
     for oname, s, defs in UNITS:

@@ -85,8 +85,10 @@ int pl_plan_create(pl_plan** out, int32_t n, const uint8_t* frozen_mask, int32_t
         pl::set_error("pl_plan_create: unknown f_mode");
         return PL_EINVAL;
     }
-    if (!(llr_max > 0.0f)) {
-        pl::set_error("pl_plan_create: llr_max must be positive");
+    if (!(llr_max > 0.0f) || (list_size > 1 && !(llr_max <= 700.0f))) {
+        // list decoders: the metric penalty log(1 + exp(z)) is evaluated for |z| <= 700
+        // (softplus.h); beyond that the reference's float64 exp overflows anyway
+        pl::set_error("pl_plan_create: llr_max must be positive (and <= 700 for list decoding)");
         return PL_EINVAL;
     }
     pl_plan* p = new pl_plan();

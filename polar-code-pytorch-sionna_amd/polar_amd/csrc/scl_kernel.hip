@@ -34,6 +34,7 @@
 
 #include "../../../include/polar_mi355x.h"
 #include "plan.h"
+#include "softplus.h"
 
 namespace {
 
@@ -237,8 +238,8 @@ __device__ void leaf(St& t, int i, bool info, int lane) {
         double l = read_alpha<FM>(t, lane, 0, i, 0);
         l = fmax(fmin(l, t.lmax), -t.lmax);
         pmv = t.pm[lane];
-        pen0 = log(1.0 + exp(-(1.0 * l)));
-        pen1 = info ? log(1.0 + exp(-(-1.0 * l))) : 0.0;
+        pen0 = pl::softplus_pm(-(1.0 * l));
+        pen1 = info ? pl::softplus_pm(-(-1.0 * l)) : 0.0;
     }
     if (!info) {
         if (lane < t.L) t.pm[lane] = pmv + pen0;
@@ -259,7 +260,7 @@ __device__ double node_softplus_sum(St& t, int p, int s, int pos, double sg) {
     double* T = t.A + p * t.half;
     for (int j = 0; j < len; ++j) {
         const double l = fmax(fmin(sg * read_alpha<FM>(t, p, s, pos, j), t.lmax), -t.lmax);
-        T[j] = log(1.0 + exp(-l));
+        T[j] = pl::softplus_pm(-l);
     }
     if (len < 8) {
         double r = 0.0;

@@ -38,6 +38,7 @@
 
 #include "../../../include/polar_mi355x.h"
 #include "plan.h"
+#include "softplus.h"
 
 namespace {
 
@@ -583,7 +584,7 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
 #if PL_SCL_DIAG_CHEAP_PEN  // timing diagnostic only (wrong metrics)
         const double pen = fmax(-sl, 0.0);
 #else
-        const double pen = log(1.0 + exp(-sl));
+        const double pen = pl::softplus_pm(-sl);
 #endif
         if (!info) {  // frozen leaf: metric update only (u = 0)
             pm = pm + pen;

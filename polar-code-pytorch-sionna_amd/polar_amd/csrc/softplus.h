@@ -1,0 +1,73 @@
+// softplus.h -- the SCL path-metric penalty log(1 + exp(z)) in fp64 (x_run_sn_polar/polar/
+// polar_scl.py:83 computes np.log(1 + np.exp(-(1-2u) * clip(llr))) in float64).
+//
+// Shared by scl_kernel.hip and scl_tree_kernel.hip so the two kernels produce identical metrics.
+// Same three roundings as the reference -- e = exp(z), y = 1 + e, log(y) -- with exp and log
+// evaluated for the range the decoder uses instead of through ocml's general routines:
+//   exp: z = k ln2 + r (Cody-Waite, two-part ln2 with FMA), |r| <= ln2/2, Taylor polynomial of
+//        degree 13 (truncation < 5e-18 relative), scaled by 2^k;
+//   log: y = 2^e m, m in [sqrt(1/2), sqrt(2)), log m = 2 atanh(s), s = (m-1)/(m+1), |s| < 0.1716,
+//        series through s^25 (truncation < 1e-18 relative).
+// Both are within ~2 ulp of the correctly rounded result, like ocml's and numpy's.  Valid for
+// |z| <= 700: pl_plan_create rejects list plans with llr_max > 700.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace pl {
+
+__device__ __forceinline__ double pm_exp(double z) {
+    constexpr double kLog2e = 1.4426950408889634;
+    constexpr double kLn2Hi = 0x1.62e42fefa39efp-1, kLn2Lo = 0x1.abc9e3b39803fp-56;
+    const double k = __builtin_rint(z * kLog2e);
+    double r = fma(-k, kLn2Hi, z);
+    r = fma(-k, kLn2Lo, r);
+    // 1/i!, i = 13 .. 0
+    double p = 1.6059043836821613e-10;
+    p = fma(p, r, 2.08767569878681e-09);
+    p = fma(p, r, 2.505210838544172e-08);
+    p = fma(p, r, 2.755731922398589e-07);
+    p = fma(p, r, 2.7557319223985893e-06);
+    p = fma(p, r, 2.48015873015873e-05);
+    p = fma(p, r, 0.0001984126984126984);
+    p = fma(p, r, 0.001388888888888889);
+    p = fma(p, r, 0.008333333333333333);
+    p = fma(p, r, 0.041666666666666664);
+    p = fma(p, r, 0.16666666666666666);
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    return ldexp(p, (int)k);
+}
+
+__device__ __forceinline__ double pm_log(double y) {  // y >= 1, finite
+    constexpr double kLn2Hi = 0x1.62e42fefa39efp-1, kLn2Lo = 0x1.abc9e3b39803fp-56;
+    double m = __builtin_amdgcn_frexp_mant(y);  // [0.5, 1)
+    int e = __builtin_amdgcn_frexp_exp(y);
+    if (m < 0.70710678118654752) {
+        m = m + m;
+        e -= 1;
+    }
+    const double f = m - 1.0;  // exact (Sterbenz)
+    const double s = f / (2.0 + f);
+    const double z = s * s;
+    // R(z) = sum_{i>=1} 2/(2i+1) z^(i-1), i = 1 .. 12
+    double R = 2.0 / 25.0;
+    R = fma(R, z, 2.0 / 23.0);
+    R = fma(R, z, 2.0 / 21.0);
+    R = fma(R, z, 2.0 / 19.0);
+    R = fma(R, z, 2.0 / 17.0);
+    R = fma(R, z, 2.0 / 15.0);
+    R = fma(R, z, 2.0 / 13.0);
+    R = fma(R, z, 2.0 / 11.0);
+    R = fma(R, z, 2.0 / 9.0);
+    R = fma(R, z, 2.0 / 7.0);
+    R = fma(R, z, 2.0 / 5.0);
+    R = fma(R, z, 2.0 / 3.0);
+    const double lm = fma(s * z, R, s + s);  // log m = 2s + s z R(z)
+    const double de = (double)e;
+    return fma(de, kLn2Hi, fma(de, kLn2Lo, lm));
+}
+
+__device__ __forceinline__ double softplus_pm(double z) { return pm_log(1.0 + pm_exp(z)); }
+
+}  // namespace pl
