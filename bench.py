@@ -187,7 +187,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32" if a.decoder == "sc" else "f64",  # SCL: fp64 LLRs and metrics (polar_scl.py:190-192)
             "data": f"synthetic AWGN LLRs, Eb/N0={a.ebno} dB, QPSK, generated on device (seed 42+rank)",
             "config": {"workload": f"{a.decoder.upper()} decode (k={k}, n={n}), bs={bs} per GPU"
                                    + (f", L={L}" if L > 1 else ""),
