@@ -128,7 +128,13 @@ std::vector<uint8_t> node_types(int n, const uint8_t* frozen) {
     return nt;
 }
 
-int static_log_g(int log_n) { return log_n > 7 ? log_n - 7 : 0; }
+// log2(lanes per codeword): n/128 lanes (8 at n = 1024), except min-sum n = 1024, which runs 16
+// lanes per codeword at 3 waves/SIMD (same-process A/B on MI355X, (512,1024) bs=65536: 0.1144 vs
+// 0.1177 ms, tools/static_probe.py)
+int static_log_g(int log_n, int f_mode) {
+    if (log_n == 10 && f_mode == PL_F_MINSUM) return 4;
+    return log_n > 7 ? log_n - 7 : 0;
+}
 
 // Lane of the codeword group holding residue r (mirror-butterfly layout of sc_static.h).
 int mirror_lane(int G, int r) {
@@ -137,9 +143,10 @@ int mirror_lane(int G, int r) {
 }
 
 std::string static_source(int n, const uint8_t* frozen, int f_mode) {
-    const int log_n = log2_exact(n), lg = static_log_g(log_n);
+    const int log_n = log2_exact(n), lg = static_log_g(log_n, f_mode);
     const std::vector<uint8_t> nt = node_types(n, frozen);
     std::ostringstream o;
+    if (lg == 4 && log_n == 10) o << "#define PL_SC_MINW 3\n";  // 16 lanes per codeword: 3 waves/SIMD
     // PL_SC_DEFINES="NAME=VALUE ..." overrides the kernel's tuning macros (development variants;
     // part of the source, hence of the cache key)
     if (const char* defs = getenv("PL_SC_DEFINES")) {
@@ -234,7 +241,7 @@ int attach_static(pl_plan* p, const uint8_t* frozen, bool allow_compile) {
     hipFunction_t f32, u8;
     r = check_hip(hipModuleGetFunction(&f32, mod, "pl_sc_static_f32"), "hipModuleGetFunction");
     if (!r) r = check_hip(hipModuleGetFunction(&u8, mod, "pl_sc_static_u8"), "hipModuleGetFunction");
-    const int G = 1 << static_log_g(p->log_n);
+    const int G = 1 << static_log_g(p->log_n, p->f_mode);
     std::vector<int32_t> loc;
     for (int i = 0; i < p->n; ++i)
         if (!frozen[i]) loc.push_back((mirror_lane(G, i % G) << 8) | (i / G));
@@ -277,7 +284,7 @@ void detach_static(pl_plan* p) {
 
 int launch_sc_static(const pl_plan* p, const float* llr, int64_t bs, void* out, int out_kind, hipStream_t st) {
     if (bs == 0 || p->k == 0) return PL_OK;
-    const int G = 1 << static_log_g(p->log_n);
+    const int G = 1 << static_log_g(p->log_n, p->f_mode);
     const int64_t per_block = 4 * (64 / G);  // pls::kWaves codeword groups of 64/G
     int64_t blocks = (bs + per_block - 1) / per_block;
     if (p->sc_persistent && p->resident_blocks > 0 && blocks > p->resident_blocks) blocks = p->resident_blocks;

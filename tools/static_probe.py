@@ -27,7 +27,12 @@ def ntable(mask):
             nt[(n >> s) + (p >> s)] = t
     return nt
 
-def lg_of(n):
+def lg_of(n, name=None):
+    """log2(lanes per codeword): the library's rule (n/128), or PROBE_LG / a name ending in _lgK."""
+    if name and "_lg" in name:
+        return int(name.rsplit("_lg", 1)[1])
+    if os.environ.get("PROBE_LG"):
+        return int(os.environ["PROBE_LG"])
     logn = n.bit_length() - 1
     return logn - 7 if logn > 7 else 0
 
@@ -36,13 +41,13 @@ def lam(G):
     h = lam(G // 2)
     return h + [G - 1 - x for x in h]
 
-def info_loc(mask):
-    n = len(mask); G = 1 << lg_of(n); L = lam(G)
+def info_loc(mask, name=None):
+    n = len(mask); G = 1 << lg_of(n, name); L = lam(G)
     pos = np.nonzero(mask == 0)[0]
     return np.array([(L[p % G] << 8) | (p // G) for p in pos], dtype=np.int32)
 
-def code_src(mask, fm=0):
-    n = len(mask); logn = n.bit_length() - 1; lg = lg_of(n)
+def code_src(mask, fm=0, name=None):
+    n = len(mask); logn = n.bit_length() - 1; lg = lg_of(n, name)
     nt = ntable(mask)
     return (f"struct PlCode {{ static constexpr int N = {n}, LOG_N = {logn}, LOG_G = {lg}, G = {1<<lg}, NS = {n>>lg}, FM = {fm};\n"
             f"  static constexpr unsigned char NT[{2*n}] = {{{','.join(map(str, nt))}}}; }};\n")
@@ -55,7 +60,7 @@ def build(k, n, name, flags):
     mask = polar_amd.frozen_mask(fp, n)
     os.makedirs(OUT, exist_ok=True)
     src = os.path.join(OUT, f"st_{name}.hip")
-    open(src, "w").write('#include "sc_static.h"\n' + code_src(mask) + "PL_SC_STATIC_KERNELS(PlCode)\n" + r'''
+    open(src, "w").write('#include "sc_static.h"\n' + code_src(mask, 0, name) + "PL_SC_STATIC_KERNELS(PlCode)\n" + r'''
 extern "C" int st_launch(const float* llr, long bs, void* out, const int* info_loc, int k, float lmax, void* st, long pf) {
     const long per = (long)pls::kWaves * (64 / PlCode::G);
     long blocks = (bs + per - 1) / per;
@@ -98,6 +103,7 @@ def run(k, n, names):
     t_ref = tm(lambda: ops.sc_decode(plan, llr, out=ref_out))
     print(f"library kernel ({k},{n}) bs={bs}: {t_ref:.4f} ms  {bs / t_ref / 1e3:.1f} Mcw/s", flush=True)
     for name in names:
+        iloc = torch.from_numpy(info_loc(mask, name)).to(dev)
         L = ctypes.CDLL(os.path.join(OUT, f"st_{name}.so"))
         L.st_launch.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_long]
         pfs = [int(v) for v in os.environ.get("PROBE_PF", "0").split(",")]
