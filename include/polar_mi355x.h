@@ -111,6 +111,11 @@ int pl_plan_kernel(const pl_plan* plan, int32_t* kind, char* path, size_t path_l
  * kernels of known codes. */
 int pl_sc_specialize(int32_t n, const uint8_t* frozen_mask, int32_t f_mode, const char* cache_dir,
                      char* path, size_t path_len);
+/* The HIP source of the specialised SC kernel of a code and its cache file name (what
+ * pl_sc_specialize would compile and look up), for compiling it out of process (hipcc --genco;
+ * polar_amd/build.py).  *src_size = bytes needed including the NUL; src may be NULL. */
+int pl_sc_source(int32_t n, const uint8_t* frozen_mask, int32_t f_mode, char* src, size_t src_len,
+                 size_t* src_size, char* name, size_t name_len);
 
 /* 5G NR data path (polar_amd/polar5g.py builds the tables on the host, 3GPP TS 38.212 5.4.1).
  * All pointers are device pointers; rows are contiguous fp32.

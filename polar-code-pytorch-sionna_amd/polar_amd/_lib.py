@@ -41,13 +41,16 @@ def _declare(L):
     L.pl_plan_kernel.argtypes = [P, P, ctypes.c_char_p, ctypes.c_size_t]
     L.pl_plan_set_crc.argtypes = [P, i32, u32]
     L.pl_sc_specialize.argtypes = [i32, P, i32, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
+    L.pl_sc_source.argtypes = [i32, P, i32, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
+                               ctypes.c_char_p, ctypes.c_size_t]
     L.pl_crc_attach.argtypes = [P, i64, i32, P, i32, P, P]
     L.pl_gather_rows.argtypes = [P, i64, i32, P, i32, P, P]
     L.pl_rate_recover.argtypes = [P, i64, i32, P, P, P, i32, P, P]
     L.pl_last_error_string.restype = ctypes.c_char_p
     L.pl_version.restype = ctypes.c_char_p
     for f in (L.pl_plan_create, L.pl_plan_destroy, L.pl_plan_info, L.pl_sc_decode, L.pl_scl_decode,
-              L.pl_polar_encode, L.pl_plan_kernel, L.pl_sc_specialize, L.pl_plan_set_crc, L.pl_crc_attach,
+              L.pl_polar_encode, L.pl_plan_kernel, L.pl_sc_specialize, L.pl_sc_source, L.pl_plan_set_crc,
+              L.pl_crc_attach,
               L.pl_gather_rows, L.pl_rate_recover):
         f.restype = ctypes.c_int
     return L
@@ -69,7 +72,8 @@ def lib():
 
 EXPORTED_SYMBOLS = ("pl_plan_create", "pl_plan_destroy", "pl_plan_info", "pl_sc_decode",
                     "pl_scl_workspace_size", "pl_scl_decode", "pl_polar_encode",
-                    "pl_plan_kernel", "pl_sc_specialize", "pl_plan_set_crc", "pl_crc_attach", "pl_gather_rows",
+                    "pl_plan_kernel", "pl_sc_specialize", "pl_sc_source", "pl_plan_set_crc", "pl_crc_attach",
+                    "pl_gather_rows",
                     "pl_rate_recover", "pl_last_error_string", "pl_version")
 
 
@@ -85,6 +89,92 @@ def current_stream_ptr(device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
+# ---- code-specialised SC kernels, compiled out of process --------------------------------------
+# The library can compile a specialised kernel itself (hiprtc, pl_sc_specialize), but in a
+# process that has imported torch, hiprtc runs against torch's bundled amd_comgr (an older ROCm
+# than /opt/rocm's hiprtc): measured here, that combination emits ~15 % more instructions for
+# the (512,1024) kernel and segfaults on at least one reference code.  So the Python layer
+# compiles with hipcc --genco in a child process (build.py ahead of time; Plan() for codes not
+# pre-built) and hands the library only cached code objects (PL_PLAN_CACHE_ONLY).
+HIPCC_GENCO = ["--offload-arch=gfx950", "--genco", "--no-gpu-bundle-output", "-O3", "-std=c++17",
+               "-ffp-contract=off"]
+
+
+def sc_source(n, frozen_mask_u8, f_mode):
+    """(HIP source, cache file name) of the specialised SC kernel of a code (pl_sc_source)."""
+    import numpy as np
+    mask = np.ascontiguousarray(frozen_mask_u8, dtype=np.uint8)
+    size, name = ctypes.c_size_t(), ctypes.create_string_buffer(256)
+    ptr = mask.ctypes.data_as(ctypes.c_void_p)
+    check(lib().pl_sc_source(int(n), ptr, int(f_mode), None, 0, ctypes.byref(size), name, 256), "pl_sc_source")
+    buf = ctypes.create_string_buffer(size.value)
+    check(lib().pl_sc_source(int(n), ptr, int(f_mode), buf, size.value, ctypes.byref(size), name, 256),
+          "pl_sc_source")
+    return buf.value.decode(), name.value.decode()
+
+
+def kernel_cache_dirs():
+    """The library's lookup order (jit.cpp cache_dirs): $PL_KERNEL_CACHE, <lib dir>/kcache,
+    ~/.cache/polar_mi355x."""
+    dirs = []
+    if os.environ.get("PL_KERNEL_CACHE"):
+        dirs.append(os.environ["PL_KERNEL_CACHE"])
+    dirs.append(os.path.join(_HERE, "kcache"))
+    if os.environ.get("HOME"):
+        dirs.append(os.path.join(os.environ["HOME"], ".cache", "polar_mi355x"))
+    return dirs
+
+
+def hipcc_path():
+    import shutil
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    return None
+
+
+def compile_code_object(src, out_dir, name, timeout=600):
+    """hipcc --genco of one specialised kernel into out_dir/name (atomic rename).  True on success."""
+    import subprocess
+    import tempfile
+    hipcc = hipcc_path()
+    if hipcc is None:
+        return False
+    os.makedirs(out_dir, exist_ok=True)
+    with tempfile.TemporaryDirectory(prefix="pl_sc_") as td:
+        hip = os.path.join(td, "pl_sc_static.hip")
+        with open(hip, "w") as f:
+            f.write(src)
+        tmp = os.path.join(td, name)
+        r = subprocess.run([hipcc, *HIPCC_GENCO, hip, "-o", tmp], capture_output=True, text=True, timeout=timeout)
+        if r.returncode != 0 or not os.path.exists(tmp):
+            return False
+        part = os.path.join(out_dir, f".{name}.{os.getpid()}.part")
+        import shutil
+        shutil.copyfile(tmp, part)
+        os.replace(part, os.path.join(out_dir, name))
+    return True
+
+
+def ensure_sc_kernel(n, frozen_mask_u8, f_mode):
+    """Make sure the specialised SC kernel of a code is in a kernel cache; compile it with hipcc
+    in a child process if not.  Returns False when it could not be provided (the plan then runs
+    the generic HIP kernel)."""
+    src, name = sc_source(n, frozen_mask_u8, f_mode)
+    dirs = kernel_cache_dirs()
+    if any(os.path.exists(os.path.join(d, name)) for d in dirs):
+        return True
+    targets = ([dirs[0]] if os.environ.get("PL_KERNEL_CACHE") else []) + \
+        [d for d in dirs if d.endswith("polar_mi355x")] + [os.path.join(_HERE, "kcache")]
+    for d in targets:
+        try:
+            if compile_code_object(src, d, name):
+                return True
+        except (OSError, ValueError):
+            pass
+    return False
+
+
 class Plan:
     """Owning wrapper of a pl_plan* (immutable, usable from any stream)."""
 
@@ -94,6 +184,11 @@ class Plan:
         import numpy as np
         mask = np.ascontiguousarray(frozen_mask_u8, dtype=np.uint8)
         assert mask.shape == (n,)
+        if int(list_size) == 1 and os.environ.get("PL_SC_SPECIALIZE") != "0" and \
+                not (flags & (PL_PLAN_GENERIC | PL_PLAN_CACHE_ONLY)):
+            # the library only loads cached code objects; compile out of process when missing
+            ensure_sc_kernel(n, mask, f_mode)
+            flags |= PL_PLAN_CACHE_ONLY
         self._h = ctypes.c_void_p()
         check(lib().pl_plan_create(ctypes.byref(self._h), int(n), mask.ctypes.data_as(ctypes.c_void_p),
                                    int(list_size), int(f_mode), float(llr_max), int(flags)), "pl_plan_create")

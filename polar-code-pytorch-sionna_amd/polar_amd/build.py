@@ -10,7 +10,7 @@ import os
 import shutil
 import subprocess
 import sys
-from concurrent.futures import ProcessPoolExecutor, ThreadPoolExecutor
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
@@ -88,39 +88,51 @@ def build(force=False, verbose=False):
     return LIB
 
 
-def _specialize_one(args):
-    """Worker: compile one code's specialised SC kernel into KCACHE (fresh process, no GPU)."""
-    import ctypes
-    import numpy as np
-    n, mask_bytes, f_mode = args
-    L = ctypes.CDLL(LIB)
-    L.pl_sc_specialize.argtypes = [ctypes.c_int32, ctypes.c_char_p, ctypes.c_int32, ctypes.c_char_p,
-                                   ctypes.c_char_p, ctypes.c_size_t]
-    L.pl_last_error_string.restype = ctypes.c_char_p
-    buf = ctypes.create_string_buffer(4096)
-    rc = L.pl_sc_specialize(n, mask_bytes, f_mode, KCACHE.encode(), buf, 4096)
-    if rc != 0:
-        return False, f"n={n} f_mode={f_mode}: {L.pl_last_error_string().decode(errors='replace')[:500]}"
-    return True, os.path.basename(buf.value.decode())
-
-
 def prebuild_codes(codes, workers=None, prune=True):
     """Compile the specialised SC kernels of `codes` = [(frozen_mask uint8[n], f_mode)] into
-    KCACHE (content-addressed: unchanged codes are found and skipped)."""
+    KCACHE with hipcc --genco, one child process per code (content-addressed names from
+    pl_sc_source: unchanged codes are found and skipped).  Not hiprtc: in a process that has
+    imported torch, hiprtc runs against torch's bundled amd_comgr (see _lib.py)."""
+    from . import _lib
     os.makedirs(KCACHE, exist_ok=True)
-    jobs = [(len(m), bytes(bytearray(m)), int(fm)) for m, fm in codes]
+    jobs, keep = [], set()
+    for m, fm in codes:
+        src, name = _lib.sc_source(len(m), m, int(fm))
+        keep.add(name)
+        if not os.path.exists(os.path.join(KCACHE, name)):
+            jobs.append((len(m), src, name))
     jobs.sort(key=lambda j: -j[0])  # longest compiles first
     workers = workers or min(8, os.cpu_count() or 1)
-    with ProcessPoolExecutor(max_workers=workers) as ex:
-        res = list(ex.map(_specialize_one, jobs))
-    errs = [v for ok, v in res if not ok]
+
+    def one(job):
+        n, src, name = job
+        return _lib.compile_code_object(src, KCACHE, name), f"n={n} {name}"
+    with ThreadPoolExecutor(max_workers=workers) as ex:
+        res = list(ex.map(one, jobs))
+    errs = [what for ok, what in res if not ok]
     if errs:
-        raise RuntimeError("specialised SC kernel pre-build failed:\n" + "\n".join(errs))
+        raise RuntimeError("specialised SC kernel pre-build (hipcc --genco) failed:\n" + "\n".join(errs))
     if prune:  # drop code objects of older kernel versions (they would only travel as dead weight)
-        keep = {v for ok, v in res if ok}
         for f in os.listdir(KCACHE):
             if f.endswith(".co") and f not in keep:
                 os.remove(os.path.join(KCACHE, f))
+
+
+def test_random_codes():
+    """The arbitrary frozen sets tests/test_sc_gpu.py::test_sc_random_vs_oracle decodes with the
+    specialised kernel (n <= 256, same seeds), so the GPU tests never compile."""
+    import numpy as np
+    out = []
+    for log_n in range(1, 9):
+        for rate in (0.25, 0.5, 0.75):
+            n = 1 << log_n
+            rng = np.random.default_rng(log_n * 10 + int(rate * 4))
+            k = max(1, int(n * rate))
+            fp = np.sort(rng.permutation(n)[: n - k])
+            m = np.zeros(n, dtype=np.uint8)
+            m[fp] = 1
+            out.append((m, 0))
+    return out
 
 
 # 5G NR (k, E) configurations the package's tests decode (tests/test_polar5g_gpu.py); their
@@ -165,6 +177,7 @@ def reference_codes():
     import io
     with contextlib.redirect_stdout(io.StringIO()):  # the CRC6 warning of 12 <= k <= 19
         out += polar5g_codes()
+    out += test_random_codes()
     uniq = {}
     for m, fm in out:
         uniq[(bytes(bytearray(m)), fm)] = (m, fm)

@@ -129,8 +129,8 @@ std::vector<uint8_t> node_types(int n, const uint8_t* frozen) {
 }
 
 // log2(lanes per codeword): n/128 lanes (8 at n = 1024), except min-sum n = 1024, which runs 16
-// lanes per codeword at 3 waves/SIMD (same-process A/B on MI355X, (512,1024) bs=65536: 0.1144 vs
-// 0.1177 ms, tools/static_probe.py)
+// lanes per codeword at 3 waves/SIMD with the v_bitop3 sign merge in f (same-process A/B on
+// MI355X, (512,1024) bs=65536: 0.1087 ms vs 0.1177 ms for n/128 lanes, tools/static_probe.py)
 int static_log_g(int log_n, int f_mode) {
     if (log_n == 10 && f_mode == PL_F_MINSUM) return 4;
     return log_n > 7 ? log_n - 7 : 0;
@@ -146,7 +146,8 @@ std::string static_source(int n, const uint8_t* frozen, int f_mode) {
     const int log_n = log2_exact(n), lg = static_log_g(log_n, f_mode);
     const std::vector<uint8_t> nt = node_types(n, frozen);
     std::ostringstream o;
-    if (lg == 4 && log_n == 10) o << "#define PL_SC_MINW 3\n";  // 16 lanes per codeword: 3 waves/SIMD
+    if (lg == 4 && log_n == 10)  // 16 lanes per codeword: 3 waves/SIMD, v_bitop3 sign merge in f
+        o << "#define PL_SC_MINW 3\n#define PL_SC_F_BITOP3 1\n";  // (A/B: 0.1087 vs 0.1140 ms)
     // PL_SC_DEFINES="NAME=VALUE ..." overrides the kernel's tuning macros (development variants;
     // part of the source, hence of the cache key)
     if (const char* defs = getenv("PL_SC_DEFINES")) {
@@ -318,6 +319,29 @@ int pl_sc_specialize(int32_t n, const uint8_t* frozen_mask, int32_t f_mode, cons
     if (path_out && path_len) {
         strncpy(path_out, path.c_str(), path_len - 1);
         path_out[path_len - 1] = 0;
+    }
+    return PL_OK;
+}
+
+int pl_sc_source(int32_t n, const uint8_t* frozen_mask, int32_t f_mode, char* src_out, size_t src_len,
+                 size_t* src_size, char* name_out, size_t name_len) {
+    if (!frozen_mask || log2_exact(n) < 1 || log2_exact(n) > 11 || (f_mode != PL_F_MINSUM && f_mode != PL_F_EXACT)) {
+        pl::set_error("pl_sc_source: bad arguments");
+        return PL_EINVAL;
+    }
+    const std::string src = pl::static_source(n, frozen_mask, f_mode);
+    const std::string name = pl::cache_name(src);
+    if (src_size) *src_size = src.size() + 1;
+    if (src_out && src_len) {
+        if (src_len < src.size() + 1) {
+            pl::set_error("pl_sc_source: source buffer too small");
+            return PL_EINVAL;
+        }
+        memcpy(src_out, src.c_str(), src.size() + 1);
+    }
+    if (name_out && name_len) {
+        strncpy(name_out, name.c_str(), name_len - 1);
+        name_out[name_len - 1] = 0;
     }
     return PL_OK;
 }

@@ -15,7 +15,8 @@
 // llr <= 0 (:90-98), partial sums [uL^uR, uR] (:83-89).  FM = 1 selects the exact boxplus f of
 // my_sn/fec/polar/dec.py:39-43 (shortcuts limited to rate-0 and repetition nodes there).
 //
-// Layout ("mirror butterfly").  A wave64 decodes 64/G codewords, G = max(1, n/128) lanes each.
+// Layout ("mirror butterfly").  A wave64 decodes 64/G codewords, G = max(1, n/128) lanes each
+// (G = 16 for min-sum n = 1024, jit.cpp static_log_g).
 // Element i of a stage buffer lives in slot i/G of the lane holding residue i mod G.  Residues
 // are placed so that the two residues an f/g pairs at every level of the bottom of the tree
 // (r and r + S/2 inside a size-S block, S <= G) sit in lanes q and q ^ (S-1): the "mirror" of a
@@ -155,6 +156,11 @@ __device__ __forceinline__ uint32_t bit31(W w, int j) {
 __device__ __forceinline__ uint32_t hd31(float x) { return (x > 0.0f) ? 0u : 0x80000000u; }
 __device__ __forceinline__ uint32_t hd(float x) { return (x > 0.0f) ? 0u : 1u; }
 
+// wave-wide "any lane": the ballot builtin directly (hiprtc's __any materialises the predicate
+// as 0/1 and compares it again: +400 VALU and +300 branches at (512,1024))
+__device__ __forceinline__ bool any_lane(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
+__device__ __forceinline__ uint64_t ballot_lanes(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+
 struct Lane {
     uint32_t lom[5];  // lom[t]: all-ones if this lane holds the low element at level 2^t
     float lmax;
@@ -230,7 +236,7 @@ __device__ __forceinline__ uint32_t lnode(float a, const Lane& ln) {
         v = v + mirf<2>(v);
         return hd31(v);
     } else if constexpr (T == R1 && C::FM == 0) {
-        if (!__any(a == 0.0f)) return fu(a) & 0x80000000u;
+        if (!any_lane(a == 0.0f)) return fu(a) & 0x80000000u;
         return lsplit<C, s, P>(a, ln);
     } else if constexpr (T == SPC && C::FM == 0) {
         // magnitudes compared as integers (non-negative floats order like their bit patterns)
@@ -246,14 +252,14 @@ __device__ __forceinline__ uint32_t lnode(float a, const Lane& ln) {
         const bool eq = ab == mn;
 #if PL_SC_SPC_BALLOT
         const bool bad_lane = (ab == 0u) | ((par != 0u) & (mn >= fu(ln.lmax)));
-        const bool bad = __any(bad_lane) || multi_in_block<S>(__ballot(eq), __ballot(par != 0u));
+        const bool bad = any_lane(bad_lane) || multi_in_block<S>(ballot_lanes(eq), ballot_lanes(par != 0u));
 #else
         uint32_t cnt = eq ? 1u : 0u;
         if constexpr (s >= 4) cnt += mir<16>(cnt);
         if constexpr (s >= 3) cnt += mir<8>(cnt);
         if constexpr (s >= 2) cnt += mir<4>(cnt);
         cnt += mir<2>(cnt);
-        const bool bad = __any((ab == 0u) | ((par != 0u) & ((cnt != 1u) | (mn >= fu(ln.lmax)))));
+        const bool bad = any_lane((ab == 0u) | ((par != 0u) & ((cnt != 1u) | (mn >= fu(ln.lmax)))));
 #endif
         if (!bad) return b ^ (eq ? par : 0u);
         return lsplit<C, s, P>(a, ln);
@@ -331,7 +337,7 @@ __device__ __forceinline__ Beta<(1 << s) / C::G> node(const float (&a)[(1 << s) 
         bool z = false;
 #pragma unroll
         for (int j = 0; j < E; ++j) z |= (a[j] == 0.0f);
-        if (!__any(z)) return signs<C, E>(a);
+        if (!any_lane(z)) return signs<C, E>(a);
         return split<C, s, P>(a, ln);
     } else if constexpr (T == SPC && C::FM == 0) {
         bool z = false;
@@ -351,11 +357,11 @@ __device__ __forceinline__ Beta<(1 << s) / C::G> node(const float (&a)[(1 << s) 
         // unique minimum: no lane holds two, and no codeword group has two lanes holding one
         const bool two = (eqm & (eqm - 1)) != 0;
         const bool bad_lane = z | ((par != 0u) & (two | (mn >= fu(ln.lmax))));
-        const bool bad = __any(bad_lane) || multi_in_block<C::G>(__ballot(eqm != 0), __ballot(par != 0u));
+        const bool bad = any_lane(bad_lane) || multi_in_block<C::G>(ballot_lanes(eqm != 0), ballot_lanes(par != 0u));
 #else
         uint32_t cnt = (uint32_t)__popcll((unsigned long long)eqm);
         cnt = grp<C::LOG_G>(cnt, [](uint32_t u, uint32_t v) { return u + v; });
-        const bool bad = __any(z | ((par != 0u) & ((cnt != 1u) | (mn >= fu(ln.lmax)))));
+        const bool bad = any_lane(z | ((par != 0u) & ((cnt != 1u) | (mn >= fu(ln.lmax)))));
 #endif
         if (!bad) return par ? (BT)(b ^ eqm) : b;
         return split<C, s, P>(a, ln);

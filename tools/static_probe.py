@@ -138,6 +138,23 @@ def run(k, n, names):
             t = tm(lambda: L.st_launch(llr.data_ptr(), bs, out.data_ptr(), iloc.data_ptr(), k, 30.0, st, pf))
             print(f"static[{name}] pf={pf} ({k},{n}): {t:.4f} ms  {bs / t / 1e3:.1f} Mcw/s  exact={ok}", flush=True)
 
+    t_ref = tm(lambda: ops.sc_decode(plan, llr, out=ref_out))
+    print(f"library kernel again ({k},{n}) bs={bs}: {t_ref:.4f} ms  {bs / t_ref / 1e3:.1f} Mcw/s", flush=True)
+    fn = _lib.lib().pl_sc_decode
+    args = (plan.handle, ctypes.c_void_p(llr.data_ptr()), bs, ctypes.c_void_p(ref_out.data_ptr()), 0, st)
+    t_dir = tm(lambda: fn(*args))
+    print(f"library kernel, direct ctypes call ({k},{n}): {t_dir:.4f} ms  {bs / t_dir / 1e3:.1f} Mcw/s", flush=True)
+    import time as _t
+    small = llr[:64].contiguous(); so = torch.empty((64, k), device=dev)
+    for f_, nm in ((lambda: ops.sc_decode(plan, small, out=so), "ops.sc_decode"),
+                   (lambda: fn(plan.handle, ctypes.c_void_p(small.data_ptr()), 64, ctypes.c_void_p(so.data_ptr()), 0, st),
+                    "direct")):
+        for _ in range(100): f_()
+        torch.cuda.synchronize(); t0 = _t.perf_counter()
+        for _ in range(2000): f_()
+        t1 = _t.perf_counter(); torch.cuda.synchronize()
+        print(f"host cost per call ({nm}, bs=64): {(t1 - t0) / 2000 * 1e6:.1f} us", flush=True)
+
 if __name__ == "__main__":
     if sys.argv[1] == "build":
         k, n = int(sys.argv[2]), int(sys.argv[3])
