@@ -95,3 +95,41 @@ def test_reference_codes_are_prebuilt():
     if not os.path.isdir(b.KCACHE):
         pytest.fail("polar_amd/kcache missing (run __graft_entry__.build())")
     assert len([f for f in os.listdir(b.KCACHE) if f.endswith(".co")]) >= len(b.reference_codes())
+
+
+def test_list_plan_rejects_llr_max_above_700():
+    # the SCL metric penalty (softplus.h) is evaluated for |z| <= 700
+    import numpy as np
+    from polar_amd import _lib
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    mask = np.zeros(8, dtype=np.uint8)
+    assert L.pl_plan_create(ctypes.byref(h), 8, mask.ctypes.data_as(ctypes.c_void_p), 4, 0, 701.0, 0) == _lib.PL_EINVAL
+    assert b"700" in L.pl_last_error_string()
+
+
+def test_sc_source_and_cache_name():
+    """pl_sc_source: the specialised kernel's source embeds the code's node table, and the cache
+    name is content-addressed (same code -> same name, another code or f_mode -> another)."""
+    import numpy as np
+    import polar_amd
+    from polar_amd import _lib
+    m = polar_amd.frozen_mask(polar_amd.reference_frozen_pos(512, 1024).numpy(), 1024)
+    src, name = _lib.sc_source(1024, m, 0)
+    assert "struct PlCode" in src and "PL_SC_STATIC_KERNELS(PlCode)" in src and "N = 1024" in src
+    assert "LOG_G = 4" in src and "#define PL_SC_MINW 3" in src  # 16 lanes per codeword at min-sum n=1024
+    assert re.fullmatch(r"sc_[0-9a-f]{16}\.co", name)
+    assert _lib.sc_source(1024, m, 0)[1] == name
+    assert _lib.sc_source(1024, m, 1)[1] != name
+    m2 = m.copy()
+    m2[np.nonzero(m2 == 0)[0][0]] = 1
+    assert _lib.sc_source(1024, m2, 0)[1] != name
+
+
+def test_prebuilt_kernels_cover_the_reference_codes():
+    """build() pre-compiles (hipcc --genco) every code the reference, the bench and the GPU tests
+    use, so nothing compiles on the GPU box."""
+    from polar_amd import _lib, build
+    have = set(os.listdir(build.KCACHE)) if os.path.isdir(build.KCACHE) else set()
+    missing = [len(m) for m, fm in build.reference_codes() if _lib.sc_source(len(m), m, fm)[1] not in have]
+    assert not missing, f"{len(missing)} specialised kernels not pre-built (run __graft_entry__.build())"
