@@ -249,32 +249,34 @@ __device__ void leaf(St& t, int i, bool info, int lane) {
     select_fork(t, pmv, pen0, pen1, i, 1, lane);
 }
 
-// Sum of log(1+exp(-clip(sg*llr))) over the stage-s node at pos for path p, in numpy's pairwise
-// order (np.sum over the last axis: < 8 terms sequentially from 0; <= 128 terms with 8
-// interleaved partial sums combined ((0+1)+(2+3))+((4+5)+(6+7)); larger halves recursively).
-// The terms are staged in [0, 2^s) of path p's own stage region, which holds only stages below
-// s (dead while the node is pruned) and slot 0 (unused).
+// Terms log(1+exp(-clip(sg*llr))) of the stage-s node at pos, for paths p0 .. p0+np-1, written
+// to base[q * stride + j] (q = p - p0): every lane of the wave computes terms, not one lane per
+// path.  The staging area [0, 2^s) of a path's own stage region holds only stages below s, dead
+// while the node is pruned.
 template <int FM>
-__device__ double node_softplus_sum(St& t, int p, int s, int pos, double sg) {
+__device__ void node_terms(St& t, int s, int pos, double sg, int p0, int np, double* base, int stride, int lane) {
     const int len = 1 << s;
-    double* T = t.A + p * t.half;
-    for (int j = 0; j < len; ++j) {
-        const double l = fmax(fmin(sg * read_alpha<FM>(t, p, s, pos, j), t.lmax), -t.lmax);
-        T[j] = pl::softplus_pm(-l);
+    for (int idx = lane; idx < np * len; idx += 64) {
+        const int q = idx >> s, j = idx & (len - 1);
+        const double l = fmax(fmin(sg * read_alpha<FM>(t, p0 + q, s, pos, j), t.lmax), -t.lmax);
+        base[q * stride + j] = pl::softplus_pm(-l);
     }
+    __syncthreads();
+}
+
+// Sum of T[0, len) in numpy's pairwise order (np.sum over the last axis: < 8 terms sequentially
+// from 0; <= 128 terms with 8 interleaved partial sums combined ((0+1)+(2+3))+((4+5)+(6+7));
+// larger halves recursively -- len is a power of two, so blocks of 128 combined pairwise).
+__device__ double pairwise_sum(const double* T, int len) {
     if (len < 8) {
         double r = 0.0;
         for (int j = 0; j < len; ++j) r += T[j];
         return r;
     }
     const int blk = len < 128 ? len : 128;
-    double acc[8];  // block sums of the current level, combined pairwise (len is a power of two)
-    double lvl[8];
+    double lvl[16];
     int nl = 0;
-    double total = 0.0;
-    (void)acc;
-    // iterative balanced tree over blocks of 128 (at most 4 blocks at n <= 1024: nb <= 4)
-    const int nb = len / blk;
+    const int nb = len / blk;  // <= 16 blocks at n <= 2048
     for (int b = 0; b < nb; ++b) {
         const double* a = T + b * blk;
         double r[8];
@@ -287,21 +289,37 @@ __device__ double node_softplus_sum(St& t, int p, int s, int pos, double sg) {
         for (int i = 0; i < nl / 2; ++i) lvl[i] = lvl[2 * i] + lvl[2 * i + 1];
         nl /= 2;
     }
-    total = lvl[0];
-    return total;
+    return lvl[0];
+}
+
+// Node sum of every path into pen (lane p < L gets path p's sum).  A node larger than a path's
+// region (the root of a rate-0 / repetition code) goes one path at a time through A[0, n): no
+// stage buffer is live then.
+template <int FM>
+__device__ double node_softplus_sums(St& t, int s, int pos, double sg, int lane) {
+    const int len = 1 << s;
+    double pen = 0.0;
+    if (len <= t.half) {
+        node_terms<FM>(t, s, pos, sg, 0, t.L, t.A, t.half, lane);
+        if (lane < t.L) pen = pairwise_sum(t.A + lane * t.half, len);
+        __syncthreads();
+    } else {
+        for (int p = 0; p < t.L; ++p) {
+            node_terms<FM>(t, s, pos, sg, p, 1, t.A, 0, lane);
+            if (lane == p) pen = pairwise_sum(t.A, len);
+            __syncthreads();
+        }
+    }
+    return pen;
 }
 
 // Pruned node (fast-SCL).  Rate-0: pm += node sum (dec.py:269-280).  Repetition: candidates
 // pm + sum(u=0) / pm + sum(u=1) -> selection and fork on the whole node (dec.py:281-306).
 template <int FM>
 __device__ void pruned_node(St& t, int s, int pos, bool rep, int lane) {
-    double pmv = 0.0, pen0 = 0.0, pen1 = 0.0;
-    if (lane < t.L) {
-        pmv = t.pm[lane];
-        pen0 = node_softplus_sum<FM>(t, lane, s, pos, 1.0);
-        if (rep) pen1 = node_softplus_sum<FM>(t, lane, s, pos, -1.0);
-    }
-    __syncthreads();
+    const double pmv = lane < t.L ? t.pm[lane] : 0.0;
+    const double pen0 = node_softplus_sums<FM>(t, s, pos, 1.0, lane);
+    const double pen1 = rep ? node_softplus_sums<FM>(t, s, pos, -1.0, lane) : 0.0;
     if (!rep) {
         if (lane < t.L) t.pm[lane] = pmv + pen0;
         __syncthreads();

@@ -98,6 +98,22 @@ def test_mysn_scl_minsum_fast_is_exact_vs_oracle(pa):
         assert np.abs(pm.cpu().numpy() - wpm).max() < 1e-9
 
 
+@pytest.mark.parametrize("k", [0, 1, 2])
+def test_mysn_scl_fast_pruned_root_vs_oracle(pa, k):
+    """Fast-SCL on codes whose root is itself pruned (k = 0: rate-0 root, k = 1: repetition root;
+    k = 2: pruned children of the root), where a node sum spans the whole codeword."""
+    from polar_amd import _lib, ops
+    for n in (32, 256):
+        fp = np.arange(n - k) if k < 2 else np.setdiff1d(np.arange(n), [n // 2 - 1, n - 1])
+        rng = np.random.default_rng(n + k)
+        llr = (rng.standard_normal((29, n)) * 2 + 0.5).astype(np.float32)
+        want, wpm = oracle.scl_decode_mysn(llr, fp, 4, fast_scl=True, exact_f=False)
+        plan = _lib.Plan(n, pa.frozen_mask(fp, n), 4, _lib.PL_F_MINSUM, flags=_lib.PL_PLAN_FAST_SCL)
+        got, pm = ops.scl_decode(plan, torch.from_numpy(llr).cuda(), return_pm=True)
+        assert np.array_equal(got.cpu().numpy(), want), (k, n)
+        assert np.abs(pm.cpu().numpy() - wpm).max() < 1e-9, (k, n)
+
+
 def test_mysn_scl_crc_pick_vs_oracle(pa):
     """CRC-aided pick on CRC-carrying codewords: exact vs the oracle's pick (min-sum f, no
     transcendental differences), and the CRC raises the block success rate."""
