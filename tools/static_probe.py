@@ -25,6 +25,19 @@ def ntable(mask):
             elif S >= 2 and f[0] and not f[1:].any(): t = SPC
             else: t = GEN
             nt[(n >> s) + (p >> s)] = t
+    # PROBE_NT_MAP="3:4,1:4:16": demote node types (e.g. SPC/rate-1 -> generic recursion) for A/B,
+    # optionally only for nodes of at most / at least the given size ("3:4:16" / "3:4:-32")
+    for spec in filter(None, os.environ.get("PROBE_NT_MAP", "").split(",")):
+        f = [int(v) for v in spec.split(":")]
+        a, b = f[0], f[1]
+        lim = f[2] if len(f) > 2 else 0
+        for s in range(logn + 1):
+            S = 1 << s
+            if lim > 0 and S > lim: continue
+            if lim < 0 and S < -lim: continue
+            for p in range(0, n, S):
+                i = (n >> s) + (p >> s)
+                if nt[i] == a: nt[i] = b
     return nt
 
 def lg_of(n, name=None):
