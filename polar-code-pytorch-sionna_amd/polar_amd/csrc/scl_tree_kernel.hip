@@ -165,6 +165,21 @@ __device__ __forceinline__ void rank_rot(double cv, int gl, int lane, int& rk) {
     }
 }
 
+// Element j of the stage-s node at position pos of one path, D stages below the channel,
+// recomputed from the channel row (logits, negated here: polar_scl.py:219) and the path's
+// partial sums -- used only for the node sums of pruned fast-SCL nodes above the stored stages.
+template <int D, int FM>
+__device__ double vread(const float* ch, const uint32_t* beta, int s, int pos, int j, double lmax) {
+    if constexpr (D == 0) {
+        return (double)(-1.0f * ch[j]);
+    } else {
+        const int h = 1 << s, pp = pos & ~(2 * h - 1);
+        const double x = vread<D - 1, FM>(ch, beta, s + 1, pp, j, lmax);
+        const double y = vread<D - 1, FM>(ch, beta, s + 1, pp, j + h, lmax);
+        return pos == pp ? f_op<FM>(x, y, lmax) : g_op(x, y, getbit(beta, pp + j));
+    }
+}
+
 // One codeword's state: LDS regions and its channel row.
 struct Cw {
     double* A;        // [L][per] stage s (R <= s <= SS) of buffer b at A[b*per + 2^s - 2^R + j]
@@ -516,6 +531,25 @@ __device__ __forceinline__ void g_step(const double* inA, double* st, uint32_t p
     f_down<tz, FM>(st, lmax);
 }
 
+// g at stage tz+1 into stage tz for leaf i (tz = ctz(i)), without descending
+template <int tz>
+__device__ __forceinline__ void g_only(const double* inA, double* st, uint32_t ps, int i) {
+    constexpr int h = 1 << tz;
+    const int p0 = i - h;
+#pragma unroll
+    for (int j = 0; j < h; ++j) {
+        double x, y;
+        if constexpr (tz + 1 == R) {
+            x = inA[j];
+            y = inA[j + h];
+        } else {
+            x = st[IDX(tz + 1) + j];
+            y = st[IDX(tz + 1) + j + h];
+        }
+        st[IDX(tz) + j] = g_op(x, y, (ps >> (p0 + j)) & 1u);
+    }
+}
+
 template <int FM>
 __device__ __forceinline__ void leaf_llr(const double* inA, double* st, uint32_t ps, int i, double lmax) {
     if (i == 0) {
@@ -549,22 +583,118 @@ __device__ __forceinline__ void pull_live(double* st, int i, int src) {
     }
 }
 
+// Selection of the L best of the 2L candidates of a codeword group: group lane c holds candidate
+// c (c < L = (state c, u=0), c >= L = (state c-L, u=1)) with metric cv.  Its rank in the stable
+// (metric, index) order comes from 2L-1 in-group broadcasts; one ds_permute then sends every
+// candidate to the group lane of its rank (ranks are a permutation of [0, 2L), so every lane is
+// written exactly once), and slots >= L re-shadow slot - L.  Returns the lane's new metric, the
+// path (group index) it descends from and the bit the candidate appended.
+template <int L>
+__device__ __forceinline__ void select_2l(double cv, int gl, int gbase, int lane, double& npm, int& par,
+                                          uint32_t& bit) {
+    constexpr int GW = 2 * L;
+    const bool hi = (gl & L) != 0;
+    int rk = 0;
+#if PL_SCL_DIAG_NO_RANK  // timing diagnostic only (wrong selection)
+    if (true) {
+        rk = gl;
+    } else
+#endif
+    if constexpr (GW == 64) {
+#pragma unroll
+        for (int c = 0; c < 2 * L; ++c) {
+            const double v = readlane_d(cv, c);
+            rk += (v < cv || (v == cv && c < lane)) ? 1 : 0;
+        }
+    } else {
+        rank_rot<GW, 1>(cv, gl, lane, rk);
+    }
+    const int dst = gbase + rk;
+    const int code = (gl & (L - 1)) | (hi ? 256 : 0);
+    const long long cb = __double_as_longlong(cv);
+    int rcode = __builtin_amdgcn_ds_permute(dst << 2, code);
+    int rlo = __builtin_amdgcn_ds_permute(dst << 2, (int)(cb & 0xffffffffLL));
+    int rhi = __builtin_amdgcn_ds_permute(dst << 2, (int)(cb >> 32));
+    const int me = gbase + (gl & (L - 1));
+    rcode = bperm_i(rcode, me);
+    rlo = bperm_i(rlo, me);
+    rhi = bperm_i(rhi, me);
+    par = rcode & 255;
+    bit = (uint32_t)rcode >> 8;
+    npm = __longlong_as_double(((long long)rhi << 32) | (unsigned int)rlo);
+}
+
+// numpy's pairwise np.sum of len = 2^s terms (len < 8: sequentially from 0; up to 128: 8
+// interleaved partial sums combined ((0+1)+(2+3))+((4+5)+(6+7)); larger: blocks of 128 combined
+// pairwise), the node sums of fast-SCL (my_sn dec.py:276-280, :297-300)
+__device__ __forceinline__ double pairwise8(const double (&r)[8]) {
+    return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+}
+
+// fast-SCL node test from the frozen bits fb of a node of len positions (mask m = all ones):
+// rate-0 = all frozen (dec.py:369-372), repetition = all but the last frozen (:373-376)
+__device__ __forceinline__ int prune_kind(uint32_t fb, uint32_t m) {
+    return fb == m ? 1 : (fb == (m >> 1) ? 2 : 0);
+}
+
+// Lane-level fast-SCL descent from stage s (its input st[IDX(s)] ready) at leaf position i of
+// the subtree: a rate-0 / repetition node is not descended -- returns its stage, kind 1 rate-0 /
+// 2 repetition; otherwise f down to the leaf (returns 0, st[0] = the leaf LLR).
+template <int s, int FM>
+__device__ __forceinline__ int descend_fast(double* st, uint32_t fz, int i, double lmax, int& kind) {
+    if constexpr (s == 0) {
+        return 0;
+    } else {
+        constexpr int len = 1 << s;
+        const int kd = prune_kind((fz >> i) & ((1u << len) - 1u), (1u << len) - 1u);
+        if (kd != 0) {
+            kind = kd;
+            return s;
+        }
+        constexpr int h = len / 2;
+#pragma unroll
+        for (int j = 0; j < h; ++j) st[IDX(s - 1) + j] = f_op<FM>(st[IDX(s) + j], st[IDX(s) + j + h], lmax);
+        return descend_fast<s - 1, FM>(st, fz, i, lmax, kind);
+    }
+}
+
+// Metric term sum of a pruned lane-level node (2, 4 or 8 inputs in v[0, len)), numpy order:
+// len < 8 sequentially from 0, len = 8 as 8 partial sums combined pairwise.
+__device__ __forceinline__ double lane_node_sum(const double (&v)[8], int len, double sg, double lmax) {
+    double tt[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const double l = fmax(fmin(sg * v[j], lmax), -lmax);
+        tt[j] = pl::softplus_pm(-l);
+    }
+    if (len == 8) return pairwise8(tt);
+    double r = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if (j < len) r += tt[j];
+    return r;
+}
+
 // Decode the stage-R node at absolute position i0 for every path of every codeword of the wave
 // (group lanes < L own paths; group lanes >= L shadow lane gl - L).  pm, org: the lane's metric
-// and origin (path index inside the group).
-template <int L, int FM, int CPW>
+// and origin (path index inside the group).  FAST: fast-SCL pruning of the rate-0 / repetition
+// nodes inside the subtree (sizes 2..8; the stage-R node itself is tested by the caller).
+template <int L, int FM, int CPW, bool FAST>
 __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, uint32_t& ps, int lane) {
     constexpr int GW = 2 * L;
     const int gl = lane & (GW - 1), gbase = lane & ~(GW - 1);
+    const bool hi = (gl & L) != 0;
     const Cw w = t.cw(lane / GW);
     double st[T - 1];
     ps = 0u;
     org = gl & (L - 1);
     const double* inA = w.A + org * t.per;  // stage R sits at offset 0 of a path's region
+    int resume = 0;                          // FAST: first leaf after a pruned node
 #if PL_SCL_UNROLL
 #pragma unroll
 #endif
     for (int i = 0; i < T; ++i) {
+        if (FAST && i < resume) continue;
         if (i > 0) {  // nodes that ended at leaf i-1 (stages 1..ctz(i)): [uL ^ uR, uR] (:147-153)
             const int tz = __builtin_ctz(i);
             for (int s = 1; s <= tz; ++s) {
@@ -573,13 +703,73 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
             }
             if (tz + 1 == R) inA = w.A + org * t.per;  // the origin may have changed
         }
-        leaf_llr<FM>(inA, st, ps, i, t.lmax);
+        if constexpr (!FAST) {
+            leaf_llr<FM>(inA, st, ps, i, t.lmax);
+        } else {
+            // the node input at stage top = R-1 (leaf 0: f of the stage-R input) or ctz(i) (g of
+            // the parent's input), then the pruning descent
+            int top;
+            if (i == 0) {
+                constexpr int h = T / 2;
+#pragma unroll
+                for (int j = 0; j < h; ++j) st[IDX(R - 1) + j] = f_op<FM>(inA[j], inA[j + h], t.lmax);
+                top = R - 1;
+            } else {
+                top = __builtin_ctz(i);
+                switch (top) {
+                    case 0: g_only<0>(inA, st, ps, i); break;
+                    case 1: g_only<1>(inA, st, ps, i); break;
+                    case 2: g_only<2>(inA, st, ps, i); break;
+                    default: g_only<R - 1>(inA, st, ps, i); break;
+                }
+            }
+            int kind = 0, ps_ = 0;
+            switch (top) {
+                case 0: ps_ = 0; break;
+                case 1: ps_ = descend_fast<1, FM>(st, fz, i, t.lmax, kind); break;
+                case 2: ps_ = descend_fast<2, FM>(st, fz, i, t.lmax, kind); break;
+                default: ps_ = descend_fast<R - 1, FM>(st, fz, i, t.lmax, kind); break;
+            }
+            if (ps_ > 0) {  // pruned node of size 2^ps_ at leaf i: its input is st[IDX(ps_)]
+                double v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = 0.0;
+                switch (ps_) {
+                    case 1: v[0] = st[IDX(1)]; v[1] = st[IDX(1) + 1]; break;
+                    case 2:
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) v[j] = st[IDX(2) + j];
+                        break;
+                    default:
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) v[j] = st[IDX(3) + j];
+                        break;
+                }
+                // repetition: shadow lanes evaluate the u = 1 branch (negated LLRs, dec.py:294)
+                const double nsum = lane_node_sum(v, 1 << ps_, (kind == 2 && hi) ? -1.0 : 1.0, t.lmax);
+                const int last = i + (1 << ps_) - 1;
+                resume = last + 1;
+                if (kind == 1) {  // rate-0: the node sum replaces its leaves' updates
+                    pm = pm + nsum;
+                } else {  // repetition: 2L candidates on the node sums, bit on the last leaf
+                    double npm;
+                    int par;
+                    uint32_t bit;
+                    select_2l<L>(pm + nsum, gl, gbase, lane, npm, par, bit);
+                    pm = npm;
+                    ps = (uint32_t)bperm_i((int)ps, gbase + par) | (bit << last);
+                    org = bperm_i(org, gbase + par);
+                    inA = w.A + org * t.per;
+                    pull_live<R - 1>(st, last, gbase + par);
+                }
+                continue;
+            }
+        }
         const double l = fmax(fmin(st[0], t.lmax), -t.lmax);
         // metric update (:83): pen = log(1 + exp(-(1-2u) l)).  At an information leaf shadow
         // lanes evaluate u = 1, path lanes u = 0: one exp/log per lane gives all 2L candidates.
         // Same expression as the reference, so same rounding.
         const bool info = ((fz >> i) & 1u) == 0u;
-        const bool hi = (gl & L) != 0;
         const double sl = (info && hi) ? -1.0 * l : 1.0 * l;
 #if PL_SCL_DIAG_CHEAP_PEN  // timing diagnostic only (wrong metrics)
         const double pen = fmax(-sl, 0.0);
@@ -590,40 +780,10 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
             pm = pm + pen;
             continue;
         }
-        // Group lane c holds candidate c: c < L = (state c, u=0), c >= L = (state c-L, u=1).  Its
-        // rank in the stable (metric, index) order comes from 2L-1 in-group broadcasts; one
-        // ds_permute then sends every candidate to the group lane of its rank (ranks are a
-        // permutation of [0, 2L), so every lane is written exactly once), and slots >= L
-        // re-shadow slot - L.
-        const double cv = pm + pen;
-        int rk = 0;
-#if PL_SCL_DIAG_NO_RANK  // timing diagnostic only (wrong selection)
-        if (true) {
-            rk = gl;
-        } else
-#endif
-        if constexpr (GW == 64) {
-#pragma unroll
-            for (int c = 0; c < 2 * L; ++c) {
-                const double v = readlane_d(cv, c);
-                rk += (v < cv || (v == cv && c < lane)) ? 1 : 0;
-            }
-        } else {
-            rank_rot<GW, 1>(cv, gl, lane, rk);
-        }
-        const int dst = gbase + rk;
-        const int code = (gl & (L - 1)) | (hi ? 256 : 0);
-        const long long cb = __double_as_longlong(cv);
-        int rcode = __builtin_amdgcn_ds_permute(dst << 2, code);
-        int rlo = __builtin_amdgcn_ds_permute(dst << 2, (int)(cb & 0xffffffffLL));
-        int rhi = __builtin_amdgcn_ds_permute(dst << 2, (int)(cb >> 32));
-        const int me = gbase + (gl & (L - 1));
-        rcode = bperm_i(rcode, me);
-        rlo = bperm_i(rlo, me);
-        rhi = bperm_i(rhi, me);
-        const int par = rcode & 255;
-        const uint32_t bit = (uint32_t)rcode >> 8;
-        const double npm = __longlong_as_double(((long long)rhi << 32) | (unsigned int)rlo);
+        double npm;
+        int par;
+        uint32_t bit;
+        select_2l<L>(pm + pen, gl, gbase, lane, npm, par, bit);
         pm = npm;
         ps = (uint32_t)bperm_i((int)ps, gbase + par) | (bit << i);
         org = bperm_i(org, gbase + par);
@@ -638,7 +798,151 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
     }
 }
 
-template <int L, int V, int FM>
+// Metric term of element j of a virtual stage-s node (D = S - s stages below the channel).
+template <int D, int FM>
+__device__ __noinline__ double vterm(const float* ch, const uint32_t* bp, int s, int pos, int j, double sg,
+                                     double lmax) {
+    const double l = fmax(fmin(sg * vread<D, FM>(ch, bp, s, pos, j, lmax), lmax), -lmax);
+    return pl::softplus_pm(-l);
+}
+
+// Metric term sum (numpy pairwise order) of the stage-s node at pos for path p, with sign sg:
+// stored stage (s <= SS), or recomputed from the channel (virtual, D = S - s <= V stages).
+// Rare (pruned nodes of 16 or more positions): kept out of line.
+template <int V, int FM>
+__device__ __noinline__ double upper_node_sum(const St& t, const Cw& w, int p, int s, int pos, double sg) {
+    const int len = 1 << s;
+    const uint32_t* bp = w.beta + p * t.W;
+    const double* in = s <= t.SS ? w.A + w.sptr[p * (t.S + 1) + s] * t.per + (1 << s) - (1 << R) : nullptr;
+    const int D = t.S - s;
+    const int blk = len < 128 ? len : 128;
+    double lvl[8];
+    int nl = 0;
+    for (int b0 = 0; b0 < len; b0 += blk) {
+        double acc[8];
+        for (int i = 0; i < blk; i += 8) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int e = b0 + i + j;
+                double tj;
+                if (in) {
+                    const double l = fmax(fmin(sg * in[e], t.lmax), -t.lmax);
+                    tj = pl::softplus_pm(-l);
+                } else if (D == 0) {
+                    tj = vterm<0, FM>(w.ch, bp, s, pos, e, sg, t.lmax);
+                } else if (D == 1 || V < 2) {
+                    tj = vterm<1, FM>(w.ch, bp, s, pos, e, sg, t.lmax);
+                } else if (D == 2 || V < 3) {
+                    tj = vterm<(V >= 2 ? 2 : 1), FM>(w.ch, bp, s, pos, e, sg, t.lmax);
+                } else if (D == 3 || V < 4) {
+                    tj = vterm<(V >= 3 ? 3 : 1), FM>(w.ch, bp, s, pos, e, sg, t.lmax);
+                } else {
+                    tj = vterm<(V >= 4 ? 4 : 1), FM>(w.ch, bp, s, pos, e, sg, t.lmax);
+                }
+                acc[j] = i == 0 ? tj : acc[j] + tj;
+            }
+        }
+        lvl[nl++] = pairwise8(acc);
+    }
+    while (nl > 1) {
+        for (int i = 0; i < nl / 2; ++i) lvl[i] = lvl[2 * i] + lvl[2 * i + 1];
+        nl /= 2;
+    }
+    return lvl[0];
+}
+
+// fast-SCL type of the node of 2^s positions at pos (s >= R) from the frozen words
+__device__ __forceinline__ int node_kind(const uint32_t* __restrict__ fw, int s, int pos) {
+    if (s < 5) {
+        const uint32_t m = (1u << (1 << s)) - 1u;
+        return prune_kind((fw[pos >> 5] >> (pos & 31)) & m, m);
+    }
+    const int w0 = pos >> 5, nw = 1 << (s - 5);
+    for (int w = 0; w < nw - 1; ++w)
+        if (fw[w0 + w] != ~0u) return 0;
+    return prune_kind(fw[w0 + nw - 1], ~0u);
+}
+
+// Re-point the upper-tree state of every path to its origin path org_s[]: partial-sum words
+// before i0 and the stage owners.
+template <int L, int CPW>
+__device__ void repoint(const St& t, int i0, int lane) {
+    constexpr int LL = ilog2(L);
+    const int W = t.W, w_lim = (i0 + 31) >> 5;
+    // CPW * L = 32 (codeword, path) pairs per wave, <= 32 words each (n <= 1024)
+    constexpr int RB = 32 * 32 / 64;
+    uint32_t vb[RB];
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+        const int idx = r * 64 + lane;
+        const int cp = idx >> 5, w = idx & 31;
+        if (w < w_lim) {
+            const Cw cw = t.cw(cp >> LL);
+            vb[r] = cw.beta[cw.org_s[cp & (L - 1)] * W + w];
+        }
+    }
+    constexpr int RS = (32 * 11 + 63) / 64;
+    uint8_t vs[RS];
+    const int S1 = t.S + 1;
+#pragma unroll
+    for (int r = 0; r < RS; ++r) {
+        const int idx = r * 64 + lane;
+        if (idx < 32 * S1) {
+            const int cp = idx / S1, e = idx - cp * S1;
+            const Cw cw = t.cw(cp >> LL);
+            vs[r] = cw.sptr[cw.org_s[cp & (L - 1)] * S1 + e];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < RB; ++r) {
+        const int idx = r * 64 + lane;
+        const int cp = idx >> 5, w = idx & 31;
+        if (w < w_lim) t.cw(cp >> LL).beta[(cp & (L - 1)) * W + w] = vb[r];
+    }
+#pragma unroll
+    for (int r = 0; r < RS; ++r) {
+        const int idx = r * 64 + lane;
+        if (idx < 32 * S1) {
+            const int cp = idx / S1, e = idx - cp * S1;
+            t.cw(cp >> LL).sptr[(cp & (L - 1)) * S1 + e] = vs[r];
+        }
+    }
+    __syncthreads();
+}
+
+// A pruned fast-SCL node of 2^s >= 2^R positions at pos (kind 1 rate-0, 2 repetition): the
+// node sums replace the descent (dec.py:269-306).  Repetition: 2L candidates on the sums, the
+// paths re-pointed to their parents, and the node's partial sums x = u..u set through its last
+// 16-position chunk (the chunks before stay 0; the combines of the stages above R complete x).
+template <int L, int V, int FM, int CPW>
+__device__ void upper_prune(const St& t, int s, int pos, int kind, double& pm, int lane) {
+    constexpr int GW = 2 * L;
+    const int gl = lane & (GW - 1), gbase = lane & ~(GW - 1);
+    const bool hi = (gl & L) != 0;
+    const Cw w = t.cw(lane / GW);
+    const double sg = (kind == 2 && hi) ? -1.0 : 1.0;
+    const double nsum = upper_node_sum<V, FM>(t, w, gl & (L - 1), s, pos, sg);
+    if (kind == 1) {
+        pm = pm + nsum;
+        return;
+    }
+    double npm;
+    int par;
+    uint32_t bit;
+    select_2l<L>(pm + nsum, gl, gbase, lane, npm, par, bit);
+    pm = npm;
+    if (gl < L) w.org_s[gl] = par;
+    __syncthreads();
+    repoint<L, CPW>(t, pos, lane);
+    if (gl < L && bit) {
+        const int b = pos + (1 << s) - T;
+        w.beta[gl * t.W + (b >> 5)] |= ((1u << T) - 1u) << (b & 31);
+    }
+    __syncthreads();
+}
+
+template <int L, int V, int FM, bool FAST>
 __global__ __launch_bounds__(64)
 #if PL_SCL_WPE > 0
 __attribute__((amdgpu_waves_per_eu(PL_SCL_WPE)))
@@ -681,83 +985,56 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
 
     double pm = gl == 0 || gl == L ? 0.0 : lmax;  // :192-194 ([0, 30 x (L-1)] per half)
     const int nsub = n >> R;
-    for (int q = 0; q < nsub; ++q) {
+    int q = 0;
+    while (q < nsub) {
         const int i0 = q << R;
         // input of the stage-R node at i0: g of the node that ends the finished left sibling,
-        // then f down to stage R (stored stages only; virtual ones are recomputed on read)
-#if PL_SCL_DIAG_NO_UPPER  // timing diagnostic only
-        if (q < 0) {
-#else
+        // then f down to stage R (stored stages only; virtual ones are recomputed on read),
+        // testing every node entered for fast-SCL pruning (my_sn dec.py:367-376)
+        int top;
         if (q == 0) {
-#endif
-            for (int s = S; s > R; --s)
-                if (s - 1 <= t.SS) node_fg<L, V, FM, CPW>(t, s, 0, false, lane);
-        } else if (!PL_SCL_DIAG_NO_UPPER) {
+            top = S;
+        } else {
             const int tz = __builtin_ctz(i0);
-            if (tz <= t.SS) node_fg<L, V, FM, CPW>(t, tz + 1, i0 & ~((2 << tz) - 1), true, lane);
-            for (int s = tz; s > R; --s)
-                if (s - 1 <= t.SS) node_fg<L, V, FM, CPW>(t, s, i0, false, lane);
+            if (!PL_SCL_DIAG_NO_UPPER && tz <= t.SS)
+                node_fg<L, V, FM, CPW>(t, tz + 1, i0 & ~((2 << tz) - 1), true, lane);
+            top = tz;
         }
-        int org;
-        uint32_t ps;
-        subtree<L, FM, CPW>(t, i0, frozen_words[i0 >> 5] >> (i0 & 31), pm, org, ps, lane);
-        // re-point the upper-tree state of every path to its origin's, then store the
-        // subtree's partial sums: partial-sum words before i0 and stage owners R..SS
-        if (gl < L) {
-            mine.org_s[gl] = org;
-            mine.ps_s[gl] = ps;
-        }
-        __syncthreads();
-        const int w_i = i0 >> 5, w_lim = (i0 + 31) >> 5, off = i0 & 31;
-        // CPW * L = 32 (codeword, path) pairs per wave, <= 32 words each (n <= 1024)
-        constexpr int RB = 32 * 32 / 64;
-        uint32_t vb[RB];
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-            const int idx = r * 64 + lane;
-            const int cp = idx >> 5, w = idx & 31;
-            if (w < w_lim) {
-                const Cw cw = t.cw(cp >> LL);
-                vb[r] = cw.beta[cw.org_s[cp & (L - 1)] * W + w];
+        int pr = 0, kind = 0;
+        for (int s = top; s >= R; --s) {
+            if constexpr (FAST) {
+                kind = node_kind(frozen_words, s, i0);
+                if (kind != 0) {
+                    pr = s;
+                    break;
+                }
             }
+            if (!PL_SCL_DIAG_NO_UPPER && s > R && s - 1 <= t.SS) node_fg<L, V, FM, CPW>(t, s, i0, false, lane);
         }
-        constexpr int RS = (32 * 11 + 63) / 64;
-        uint8_t vs[RS];
-        const int S1 = S + 1;
-#pragma unroll
-        for (int r = 0; r < RS; ++r) {
-            const int idx = r * 64 + lane;
-            if (idx < 32 * S1) {
-                const int cp = idx / S1, e = idx - cp * S1;
-                const Cw cw = t.cw(cp >> LL);
-                vs[r] = cw.sptr[cw.org_s[cp & (L - 1)] * S1 + e];
+        if (FAST && kind != 0) {
+            upper_prune<L, V, FM, CPW>(t, pr, i0, kind, pm, lane);
+            q += 1 << (pr - R);
+        } else {
+            int org;
+            uint32_t ps;
+            subtree<L, FM, CPW, FAST>(t, i0, frozen_words[i0 >> 5] >> (i0 & 31), pm, org, ps, lane);
+            // re-point the upper-tree state of every path to its origin's, then store the
+            // subtree's partial sums: partial-sum words before i0 and stage owners R..SS
+            if (gl < L) mine.org_s[gl] = org;
+            __syncthreads();
+            repoint<L, CPW>(t, i0, lane);
+            const int w_i = i0 >> 5, off = i0 & 31;
+            if (gl < L) {
+                uint32_t* bw = mine.beta + gl * W + w_i;
+                *bw = off == 0 ? ps : ((*bw & ((1u << off) - 1u)) | (ps << off));
             }
+            __syncthreads();
+            q += 1;
         }
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < RB; ++r) {
-            const int idx = r * 64 + lane;
-            const int cp = idx >> 5, w = idx & 31;
-            if (w < w_lim) t.cw(cp >> LL).beta[(cp & (L - 1)) * W + w] = vb[r];
-        }
-#pragma unroll
-        for (int r = 0; r < RS; ++r) {
-            const int idx = r * 64 + lane;
-            if (idx < 32 * S1) {
-                const int cp = idx / S1, e = idx - cp * S1;
-                t.cw(cp >> LL).sptr[(cp & (L - 1)) * S1 + e] = vs[r];
-            }
-        }
-        if (T < 32 && off != 0) __syncthreads();  // the word's low part was just copied
-        if (gl < L) {
-            uint32_t* bw = mine.beta + gl * W + w_i;
-            *bw = off == 0 ? ps : ((*bw & ((1u << off) - 1u)) | (ps << off));
-        }
-        __syncthreads();
-        // nodes above R that end with this subtree
-        const int nxt = i0 + T;
-        const int top = nxt < n ? __builtin_ctz(nxt) : S;
-        for (int s = R + 1; s <= top; ++s) combine_upper<L, CPW>(t, s, nxt - (1 << s), lane);
+        // nodes above R that end here
+        const int nxt = q << R;
+        const int top2 = nxt < n ? __builtin_ctz(nxt) : S;
+        for (int s = R + 1; s <= top2; ++s) combine_upper<L, CPW>(t, s, nxt - (1 << s), lane);
     }
     if (gl < L) mine.pm_s[gl] = pm;
 
@@ -849,15 +1126,17 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
 // file once per PL_SCL_TREE_L in parallel, plus once with PL_SCL_TREE_DISPATCH for the launcher).
 namespace pl {
 template <int L>
-const void* scl_tree_fn(int v, bool exact);
+const void* scl_tree_fn(int v, bool exact, bool fast);
 }
 
 #ifdef PL_SCL_TREE_L
 namespace pl {
 template <>
-const void* scl_tree_fn<PL_SCL_TREE_L>(int v, bool exact) {
+const void* scl_tree_fn<PL_SCL_TREE_L>(int v, bool exact, bool fast) {
     constexpr int L = PL_SCL_TREE_L;
-#define PL_FM(V) (exact ? (const void*)scl_tree_kernel<L, V, 1> : (const void*)scl_tree_kernel<L, V, 0>)
+#define PL_FM(V)                                                                                  \
+    (exact ? (fast ? (const void*)scl_tree_kernel<L, V, 1, true> : (const void*)scl_tree_kernel<L, V, 1, false>) \
+           : (fast ? (const void*)scl_tree_kernel<L, V, 0, true> : (const void*)scl_tree_kernel<L, V, 0, false>))
     switch (v) {
         case 0: return PL_FM(0);
         case 1: return PL_FM(1);
@@ -887,7 +1166,9 @@ namespace pl {
 
 // Eligible plans: 2 <= L <= 32, 32 <= n <= 1024, no fast-SCL pruning.
 bool scl_tree_eligible(const pl_plan* p) {
-    if (p->flags & (PL_PLAN_FAST_SCL | PL_PLAN_GENERIC)) return false;
+    if (p->flags & PL_PLAN_GENERIC) return false;
+    if (const char* e = getenv("PL_SCL_TREE_FAST"))  // fast-SCL plans on the generic kernel (A/B)
+        if (e[0] == '0' && (p->flags & PL_PLAN_FAST_SCL)) return false;
     if (const char* e = getenv("PL_SCL_TREE"))
         if (e[0] == '0') return false;
     return p->list_size >= 2 && p->list_size <= 32 && p->log_n >= 5 && p->log_n <= 10;
@@ -902,20 +1183,21 @@ int launch_scl_tree(const pl_plan* p, const float* llr, int64_t bs, void* out, i
     }
     const int S = p->log_n, L = p->list_size, V = pick_v(S);
     const bool exact = p->f_mode == PL_F_EXACT;
+    const bool fast = (p->flags & PL_PLAN_FAST_SCL) != 0;
     const void* fn = nullptr;
 #ifdef PL_SCL_VARIANT_ONLY_L8  // development variant libraries (tools/scl_variants.py)
     if (L != 8) {
         set_error("variant library: L = 8 only");
         return PL_ENOTSUP;
     }
-    fn = scl_tree_fn<8>(V, exact);
+    fn = scl_tree_fn<8>(V, exact, fast);
 #else
     switch (L) {
-        case 2: fn = scl_tree_fn<2>(V, exact); break;
-        case 4: fn = scl_tree_fn<4>(V, exact); break;
-        case 8: fn = scl_tree_fn<8>(V, exact); break;
-        case 16: fn = scl_tree_fn<16>(V, exact); break;
-        default: fn = scl_tree_fn<32>(V, exact); break;
+        case 2: fn = scl_tree_fn<2>(V, exact, fast); break;
+        case 4: fn = scl_tree_fn<4>(V, exact, fast); break;
+        case 8: fn = scl_tree_fn<8>(V, exact, fast); break;
+        case 16: fn = scl_tree_fn<16>(V, exact, fast); break;
+        default: fn = scl_tree_fn<32>(V, exact, fast); break;
     }
 #endif
     const Lay y = make_layout(p->n, S, L, V);

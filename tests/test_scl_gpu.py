@@ -107,6 +107,36 @@ def test_scl_subtree_equals_generic(pa, log_n, L, f_mode):
         assert torch.equal(pm1, pm2), (n, L, k)
 
 
+@pytest.mark.parametrize("f_mode", [0, 1])
+@pytest.mark.parametrize("log_n", [5, 7, 9, 10])
+@pytest.mark.parametrize("L", [2, 4, 8, 16, 32])
+def test_scl_subtree_fast_equals_generic(pa, log_n, L, f_mode):
+    """Fast-SCL (my_sn use_fast_scl, dec.py:269-306) on the subtree kernel: pruned rate-0 and
+    repetition nodes at every size (inside the lane subtrees and above them, stored and virtual
+    inputs, up to the whole code) -- bits and metrics identical to the generic kernel's."""
+    from polar_amd import _lib
+    n = 1 << log_n
+    rng = np.random.default_rng(500 * log_n + L + 3 * f_mode)
+    sets = [np.sort(pa.reference_frozen_pos(n // 2, n).numpy()),   # RM-weight code: many pruned nodes
+            np.sort(rng.permutation(n)[: n - n // 4]),            # random, low rate
+            np.arange(n - 1),                                      # repetition root (k = 1)
+            np.setdiff1d(np.arange(n), [n // 2 - 1, n - 1, n // 4 - 1])]
+    for fp in sets:
+        bs = 45
+        llr = (rng.standard_normal((bs, n)) * 2.5 + 0.5).astype(np.float32)
+        llr[:6] = np.round(llr[:6])
+        llr[6:9] *= 40.0
+        x = torch.from_numpy(llr).cuda()
+        mask = pa.frozen_mask(fp, n)
+        p1 = _lib.Plan(n, mask, L, f_mode, flags=_lib.PL_PLAN_FAST_SCL)
+        p2 = _lib.Plan(n, mask, L, f_mode, flags=_lib.PL_PLAN_FAST_SCL | _lib.PL_PLAN_GENERIC)
+        assert p1.kernel()[0] == "scl_subtree" and p2.kernel()[0] == "generic"
+        b1, pm1 = pa.ops.scl_decode(p1, x, return_pm=True)
+        b2, pm2 = pa.ops.scl_decode(p2, x, return_pm=True)
+        assert torch.equal(b1, b2), (n, L, len(fp))
+        assert torch.equal(pm1, pm2), (n, L, len(fp))
+
+
 def test_scl_subtree_crc_vs_generic(pa):
     """CRC-aided pick (pl_plan_set_crc) without fast-SCL runs on the subtree kernel."""
     from polar_amd.mysn import crc_params
