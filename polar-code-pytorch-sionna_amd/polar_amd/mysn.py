@@ -5,7 +5,8 @@
                (use_fast_scl, :367-376), optional CRC-aided pick (crc_degree, :507-518)
 
 Both run in libpolar_mi355x.so on a ROCm GPU (SC: the per-code specialised kernel in exact-f mode;
-SCL: scl_kernel.hip with FM=1 / FAST / CRC).  Differences from the reference are stated where
+SCL: the subtree kernel scl_tree_kernel.hip with exact f / fast-SCL / CRC, the generic
+scl_kernel.hip for n > 1024).  Differences from the reference are stated where
 they exist:
   * The reference's CRCEncoder cannot be constructed as shipped (crc.py:81 reads self.device,
     which is never set), so SCL_Dec(crc_degree=...) raises there; here it works, with the CRC of
