@@ -55,6 +55,9 @@ namespace {
 #ifndef PL_SCL_DIAG_NO_UPPER
 #define PL_SCL_DIAG_NO_UPPER 0
 #endif
+#ifndef PL_SCL_DIAG_NO_UPPER_PRUNE
+#define PL_SCL_DIAG_NO_UPPER_PRUNE 0  // timing diagnostic: fast-SCL only inside the lane subtrees (wrong)
+#endif
 #ifndef PL_SCL_DIAG_SKIP_V
 #define PL_SCL_DIAG_SKIP_V 0
 #endif
@@ -1003,7 +1006,7 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
         int pr = 0, kind = 0;
         for (int s = top; s >= R; --s) {
             if constexpr (FAST) {
-                kind = node_kind(frozen_words, s, i0);
+                kind = PL_SCL_DIAG_NO_UPPER_PRUNE ? 0 : node_kind(frozen_words, s, i0);
                 if (kind != 0) {
                     pr = s;
                     break;

@@ -56,7 +56,9 @@ def time_all(n=1024, k=512, bs=8192, reps=5, rounds=2):
     for name, path in libs:
         L = _lib._declare(ctypes.CDLL(path))
         h = ctypes.c_void_p()
-        assert L.pl_plan_create(ctypes.byref(h), n, mask.ctypes.data_as(ctypes.c_void_p), 8, 0, 30.0, 0) == 0
+        flags = int(os.environ.get("SCL_FLAGS", "0"))  # e.g. 4 = PL_PLAN_FAST_SCL
+        fmode = int(os.environ.get("SCL_FMODE", "0"))
+        assert L.pl_plan_create(ctypes.byref(h), n, mask.ctypes.data_as(ctypes.c_void_p), 8, fmode, 30.0, flags) == 0
         handles.append((name, L, h))
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     for rnd in range(rounds):
