@@ -128,11 +128,17 @@ std::vector<uint8_t> node_types(int n, const uint8_t* frozen) {
     return nt;
 }
 
-// log2(lanes per codeword): n/128 lanes (8 at n = 1024), except min-sum n = 1024, which runs 16
-// lanes per codeword at 3 waves/SIMD with the v_bitop3 sign merge in f (same-process A/B on
-// MI355X, (512,1024) bs=65536: 0.1087 ms vs 0.1177 ms for n/128 lanes, tools/static_probe.py)
+// Min-sum codes of n = 256, 512, 1024 run n/64 lanes per codeword (instead of n/128) at 3
+// waves/SIMD, with the v_bitop3 sign merge in f, and decode their lane-level SPC nodes (size <= G)
+// by the plain recursion rather than the DPP parity/minimum shortcut.  Same-process A/B on MI355X
+// (tools/static_probe.py, bs = 65536): (512,1024) 0.1009 vs 0.1177 ms, (256,512) 0.0419 vs
+// 0.0489 ms, (128,256) 0.0230 vs 0.0411 ms; n = 128 is faster at one lane per codeword, and
+// n = 2048 already uses the widest group (16 lanes).
+bool tuned_wide(int log_n, int f_mode) { return f_mode == PL_F_MINSUM && log_n >= 8 && log_n <= 10; }
+
+// log2(lanes per codeword)
 int static_log_g(int log_n, int f_mode) {
-    if (log_n == 10 && f_mode == PL_F_MINSUM) return 4;
+    if (tuned_wide(log_n, f_mode)) return log_n - 6;
     return log_n > 7 ? log_n - 7 : 0;
 }
 
@@ -145,10 +151,9 @@ int mirror_lane(int G, int r) {
 std::string static_source(int n, const uint8_t* frozen, int f_mode) {
     const int log_n = log2_exact(n), lg = static_log_g(log_n, f_mode);
     std::vector<uint8_t> nt = node_types(n, frozen);
-    if (lg == 4 && log_n == 10) {
-        // 16 lanes per codeword: lane-level SPC nodes (size <= 16) decode faster by the plain
-        // recursion than by the DPP parity/minimum shortcut (A/B: 0.1009 vs 0.1088 ms; the
-        // in-lane SPC nodes of size >= 32 keep the shortcut)
+    if (tuned_wide(log_n, f_mode)) {
+        // lane-level SPC nodes (size <= G) by the plain recursion (A/B at n = 1024: 0.1009 vs
+        // 0.1088 ms; the in-lane SPC nodes keep the shortcut)
         for (int s = 1; s <= lg; ++s)
             for (int p = 0; p < n; p += 1 << s) {
                 uint8_t& t = nt[(size_t)(n >> s) + (size_t)(p >> s)];
@@ -156,8 +161,7 @@ std::string static_source(int n, const uint8_t* frozen, int f_mode) {
             }
     }
     std::ostringstream o;
-    if (lg == 4 && log_n == 10)  // 16 lanes per codeword: 3 waves/SIMD, v_bitop3 sign merge in f
-        o << "#define PL_SC_MINW 3\n#define PL_SC_F_BITOP3 1\n";  // (A/B: 0.1087 vs 0.1140 ms)
+    if (tuned_wide(log_n, f_mode)) o << "#define PL_SC_MINW 3\n#define PL_SC_F_BITOP3 1\n";
     // PL_SC_DEFINES="NAME=VALUE ..." overrides the kernel's tuning macros (development variants;
     // part of the source, hence of the cache key)
     if (const char* defs = getenv("PL_SC_DEFINES")) {

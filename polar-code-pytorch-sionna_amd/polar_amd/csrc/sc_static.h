@@ -16,7 +16,7 @@
 // my_sn/fec/polar/dec.py:39-43 (shortcuts limited to rate-0 and repetition nodes there).
 //
 // Layout ("mirror butterfly").  A wave64 decodes 64/G codewords, G = max(1, n/128) lanes each
-// (G = 16 for min-sum n = 1024, jit.cpp static_log_g).
+// (n/64 lanes for min-sum n = 256 .. 1024, jit.cpp static_log_g).
 // Element i of a stage buffer lives in slot i/G of the lane holding residue i mod G.  Residues
 // are placed so that the two residues an f/g pairs at every level of the bottom of the tree
 // (r and r + S/2 inside a size-S block, S <= G) sit in lanes q and q ^ (S-1): the "mirror" of a

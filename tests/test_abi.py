@@ -117,7 +117,7 @@ def test_sc_source_and_cache_name():
     m = polar_amd.frozen_mask(polar_amd.reference_frozen_pos(512, 1024).numpy(), 1024)
     src, name = _lib.sc_source(1024, m, 0)
     assert "struct PlCode" in src and "PL_SC_STATIC_KERNELS(PlCode)" in src and "N = 1024" in src
-    assert "LOG_G = 4" in src and "#define PL_SC_MINW 3" in src  # 16 lanes per codeword at min-sum n=1024
+    assert "LOG_G = 4" in src and "#define PL_SC_MINW 3" in src  # n/64 = 16 lanes per codeword at min-sum n=1024
     assert re.fullmatch(r"sc_[0-9a-f]{16}\.co", name)
     assert _lib.sc_source(1024, m, 0)[1] == name
     assert _lib.sc_source(1024, m, 1)[1] != name
