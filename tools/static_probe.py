@@ -73,7 +73,7 @@ def build(k, n, name, flags):
     mask = polar_amd.frozen_mask(fp, n)
     os.makedirs(OUT, exist_ok=True)
     src = os.path.join(OUT, f"st_{name}.hip")
-    open(src, "w").write('#include "sc_static.h"\n' + code_src(mask, 0, name) + "PL_SC_STATIC_KERNELS(PlCode)\n" + r'''
+    open(src, "w").write('#include "sc_static.h"\n' + code_src(mask, int(os.environ.get("PROBE_FM", "0")), name) + "PL_SC_STATIC_KERNELS(PlCode)\n" + r'''
 extern "C" int st_launch(const float* llr, long bs, void* out, const int* info_loc, int k, float lmax, void* st, long pf) {
     const long per = (long)pls::kWaves * (64 / PlCode::G);
     long blocks = (bs + per - 1) / per;
@@ -101,7 +101,7 @@ def run(k, n, names):
     llr = llr.contiguous()
     x2 = (torch.randn(bs, n, device=dev, generator=gen) * 2).contiguous()
     x3 = torch.round(x2 * 2) / 2  # ties and exact zeros
-    plan = _lib.Plan(n, mask, 1, 0)
+    plan = _lib.Plan(n, mask, 1, int(os.environ.get("PROBE_FM", "0")))
     iloc = torch.from_numpy(info_loc(mask)).to(dev)
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     def tm(fn, reps=20):
