@@ -810,10 +810,10 @@ __device__ __noinline__ double vterm(const float* ch, const uint32_t* bp, int s,
 }
 
 // Metric term sum (numpy pairwise order) of the stage-s node at pos for path p, with sign sg:
-// stored stage (s <= SS), or recomputed from the channel (virtual, D = S - s <= V stages).
-// Rare (pruned nodes of 16 or more positions): kept out of line.
+// stored stage (s <= SS, inline), or recomputed from the channel (virtual, D = S - s <= V
+// stages: the out-of-line vterm, scalar arguments only so nothing is passed through scratch).
 template <int V, int FM>
-__device__ __noinline__ double upper_node_sum(const St& t, const Cw& w, int p, int s, int pos, double sg) {
+__device__ __forceinline__ double upper_node_sum(const St& t, const Cw& w, int p, int s, int pos, double sg) {
     const int len = 1 << s;
     const uint32_t* bp = w.beta + p * t.W;
     const double* in = s <= t.SS ? w.A + w.sptr[p * (t.S + 1) + s] * t.per + (1 << s) - (1 << R) : nullptr;
