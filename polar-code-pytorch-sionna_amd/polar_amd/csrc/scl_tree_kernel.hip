@@ -64,6 +64,12 @@ namespace {
 #ifndef PL_SCL_DIAG_SKIP_ST
 #define PL_SCL_DIAG_SKIP_ST 0
 #endif
+#ifndef PL_SCL_FROZEN_PAIR
+#define PL_SCL_FROZEN_PAIR 1  // 1: a frozen sibling leaf pair takes one exp/log per lane (shadow lanes the right leaf)
+#endif
+#ifndef PL_SCL_RANK_MASK
+#define PL_SCL_RANK_MASK 1  // 1: 16-lane rank with a static tie mask and carry-in adds (no index DPP)
+#endif
 #ifndef PL_SCL_WPE
 #define PL_SCL_WPE 2  // > 0: amdgpu_waves_per_eu minimum (2: <= 256 VGPRs, A/B on MI355X: 2.30 vs 3.62 ms at V=4)
 #endif
@@ -144,10 +150,39 @@ __device__ __forceinline__ double dpp_d(double v) {
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// Value of group lane gl ^ L (a path lane's shadow, or a shadow lane's path).
+template <int L>
+__device__ __forceinline__ double half_xchg(double v, int lane) {
+    if constexpr (L == 8) return dpp_d<0x120 + 8>(v);  // row_ror:8 in the 16-lane row = lane ^ 8
+    else if constexpr (L == 2) return dpp_d<0x4E>(v);  // quad_perm [2,3,0,1]
+    else return bperm_d(v, lane ^ L);
+}
+
 // Candidate (metric) of group lane (gl + r) mod GW, r = 1..GW-1, accumulated into the rank of
 // this lane's candidate in the stable (metric, index) order.
+// acc + (bit `lane` of m): one v_addc with the lane mask as carry-in
+__device__ __forceinline__ int add_lane_bit(int acc, uint64_t m) {
+    int r;
+    uint64_t co;
+    asm("v_addc_co_u32_e64 %0, %1, 0, %2, %3" : "=v"(r), "=s"(co) : "v"(acc), "s"(m));
+    return r;
+}
+
 template <int GW, int r>
 __device__ __forceinline__ void rank_rot(double cv, int gl, int lane, int& rk) {
+#if PL_SCL_RANK_MASK
+    if constexpr (GW == 16 && r < GW) {
+        // row_ror:r -- group lane gl receives group lane (gl - r) mod 16, whose candidate index
+        // is the lower one exactly when gl >= r: that tie mask is a constant per rotation
+        const double v = dpp_d<0x120 + r>(cv);
+        constexpr uint64_t tie = (uint64_t)((0xFFFFu << r) & 0xFFFFu) * 0x0001000100010001ull;
+        const uint64_t lt = __builtin_amdgcn_ballot_w64(v < cv);
+        const uint64_t eq = __builtin_amdgcn_ballot_w64(v == cv);
+        rk = add_lane_bit(rk, lt | (eq & tie));
+        rank_rot<GW, r + 1>(cv, gl, lane, rk);
+        return;
+    }
+#endif
     if constexpr (r < GW) {
         double v;
         if constexpr (GW == 16) {
@@ -693,11 +728,13 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
     org = gl & (L - 1);
     const double* inA = w.A + org * t.per;  // stage R sits at offset 0 of a path's region
     int resume = 0;                          // FAST: first leaf after a pruned node
+    bool pair = false;                       // !FAST: leaf i-1 started a frozen sibling pair
 #if PL_SCL_UNROLL
 #pragma unroll
 #endif
     for (int i = 0; i < T; ++i) {
         if (FAST && i < resume) continue;
+        if (!FAST && PL_SCL_FROZEN_PAIR && (i & 1) && pair) continue;  // done with leaf i-1
         if (i > 0) {  // nodes that ended at leaf i-1 (stages 1..ctz(i)): [uL ^ uR, uR] (:147-153)
             const int tz = __builtin_ctz(i);
             for (int s = 1; s <= tz; ++s) {
@@ -768,7 +805,15 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
                 continue;
             }
         }
-        const double l = fmax(fmin(st[0], t.lmax), -t.lmax);
+        // Frozen sibling pair (leaves i, i+1 both frozen, i even): u_i = 0 is known, so the
+        // shadow lanes take leaf i+1's LLR g(a, b, 0) from the stage-1 input and the pair costs
+        // one exp/log per lane; the metric still adds the two terms in order.
+        double lv = st[0];
+        if constexpr (!FAST && PL_SCL_FROZEN_PAIR) {
+            pair = (i & 1) == 0 && ((fz >> i) & 3u) == 3u;
+            if (pair && hi) lv = g_op(st[IDX(1)], st[IDX(1) + 1], 0u);
+        }
+        const double l = fmax(fmin(lv, t.lmax), -t.lmax);
         // metric update (:83): pen = log(1 + exp(-(1-2u) l)).  At an information leaf shadow
         // lanes evaluate u = 1, path lanes u = 0: one exp/log per lane gives all 2L candidates.
         // Same expression as the reference, so same rounding.
@@ -780,7 +825,12 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
         const double pen = pl::softplus_pm(-sl);
 #endif
         if (!info) {  // frozen leaf: metric update only (u = 0)
-            pm = pm + pen;
+            if (!FAST && PL_SCL_FROZEN_PAIR && pair) {
+                const double oth = half_xchg<L>(pen, lane);
+                pm = (pm + (hi ? oth : pen)) + (hi ? pen : oth);
+            } else {
+                pm = pm + pen;
+            }
             continue;
         }
         double npm;

@@ -93,4 +93,5 @@ if __name__ == "__main__":
         ap.add_argument("--k", type=int, default=512)
         ap.add_argument("--bs", type=int, default=8192)
         a = ap.parse_args()
-        time_all(a.n, a.k, a.bs)
+        time_all(a.n, a.k, a.bs, reps=int(os.environ.get("SCL_REPS", "5")),
+                 rounds=int(os.environ.get("SCL_ROUNDS", "2")))
