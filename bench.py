@@ -116,23 +116,20 @@ def main():
     fp = polar_amd.reference_frozen_pos(k, n)
     mask = polar_amd.frozen_mask(fp, n)
     L = a.list_size if a.decoder == "scl" else 1
-    plan = _lib.Plan(n, mask, L, _lib.PL_F_MINSUM)
+    plan = _lib.Plan(n, mask, L, _lib.PL_F_MINSUM, device=dev)
     gen = torch.Generator(device=dev).manual_seed(42 + rank)
     model = channel.System_AWGN_model(n, k, channel.GpuEncoder(fp, n), None, device=dev, generator=gen)
     with torch.no_grad():
         bits, _, llr = model.llrs(bs, torch.tensor(a.ebno, dtype=torch.float32))
     llr = llr.contiguous()
     out = torch.empty((bs, k), dtype=torch.float32, device=dev)
-    ws = None
-    if a.decoder == "scl":
-        ws_bytes = int(_lib.lib().pl_scl_workspace_size(plan.handle, bs))
-        ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=dev)
+    ws = ops.scl_workspace(plan, bs, dev) if a.decoder == "scl" else None
 
     def step():
         if a.decoder == "sc":
             ops.sc_decode(plan, llr, out=out)
         else:
-            ops.scl_decode(plan, llr, out=out)
+            ops.scl_decode(plan, llr, out=out, workspace=ws)
 
     # DVFS: a cold MI355X runs the first few ms of work at a lower clock (measured: 0.127 ms/launch
     # with 3 warmup steps vs 0.119 ms after ~0.1 s of load), so settle the clock first.

@@ -9,12 +9,18 @@
  * No exceptions cross this boundary: 0 = success, negative = error, details from
  * pl_last_error_string() (thread-local).
  *
+ * Plans are device-bound: pl_plan_create allocates the plan's tables and loads its kernel module
+ * on the device current at that call (hipSetDevice).  Decode/encode calls must pass a stream of
+ * that device (or NULL with that device current); any other device gives PL_EINVAL.  Create one
+ * plan per GPU to decode on several GPUs.
+ *
  * Reference interfaces replaced (jaco267/polar-code-pytorch-sionna):
  *   pl_plan_create   SC_Dec.__init__   x_run_sn_polar/polar/polar_sc.py:10-32
  *                    SCL_Dec.__init__  x_run_sn_polar/polar/polar_scl.py:13-42
  *                    (my_sn/fec/polar/dec.py:18-31 and :183-242 for the exact-f variants)
  *   pl_sc_decode     SC_Dec.forward    x_run_sn_polar/polar/polar_sc.py:113-133
  *                    (f_mode=PL_F_EXACT: my_sn/fec/polar/dec.py:130-157)
+ *   pl_plan_info / pl_plan_device: the plan's n, k, list size (polar_sc.py:14-17) and device
  *   pl_scl_decode    SCL_Dec.forward   x_run_sn_polar/polar/polar_scl.py:210-234
  *                    (+ final sorted msg_pm of _decode_np_batch :178-209)
  *   pl_polar_encode  PolarEncoder.forward x_run_sn_polar/polar/enc.py:30-43
@@ -69,12 +75,16 @@ typedef struct pl_plan pl_plan;
  *              runs a kernel specialised to its frozen set: compiled with hiprtc at plan creation
  *              (seconds) unless a cached code object exists ($PL_KERNEL_CACHE, <library dir>/kcache,
  *              ~/.cache/polar_mi355x); PL_SC_SPECIALIZE=0 in the environment disables this.
- * n must be a power of two, 2 <= n <= 2048 (SC) / 2 <= n <= 1024 (SCL). */
+ * n must be a power of two, 2 <= n <= 2048.  List plans: list_size <= 32 for n <= 1024,
+ * list_size <= 16 at n = 2048 (the list state of one codeword must fit one CU's LDS); larger ones
+ * are rejected here with PL_ENOTSUP. */
 int pl_plan_create(pl_plan** out, int32_t n, const uint8_t* frozen_mask, int32_t list_size,
                    int32_t f_mode, float llr_max, uint32_t flags);
 int pl_plan_destroy(pl_plan* plan);
 /* n, k (information bits) and list size of a plan (any pointer may be NULL). */
 int pl_plan_info(const pl_plan* plan, int32_t* n, int32_t* k, int32_t* list_size);
+/* The HIP device the plan was created on (its tables and kernel module live there). */
+int pl_plan_device(const pl_plan* plan, int32_t* device);
 
 /* SC decode.  llr_logits: [bs, n] fp32 logits log(P(b=1)/P(b=0)) (NOT negated; the decoder
  * negates, polar_sc.py:122).  out_bits: [bs, k] decided information bits at info_pos ascending,
@@ -96,7 +106,8 @@ int pl_polar_encode(const pl_plan* plan, const float* u_bits, int64_t bs, float*
 
 /* CRC-aided SCL (my_sn/fec/polar/dec.py:507-518): after decoding, every path whose k decoded
  * bits fail the CRC (generator x^degree + sum of the bits of poly_mask, MSB-first shift register,
- * my_sn/fec/crc.py) gets +30*k on its metric before the first argmin.  degree 0 turns it off.
+ * my_sn/fec/crc.py) gets +llr_max*k on its metric (the plan's llr_max; 30 in the reference,
+ * dec.py:517) before the first argmin.  degree 0 turns it off.
  * Call before the plan's first decode.  Replaces SCL_Dec(crc_degree=...) (dec.py:210-218). */
 int pl_plan_set_crc(pl_plan* plan, int32_t degree, uint32_t poly_mask);
 

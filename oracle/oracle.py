@@ -34,7 +34,8 @@ def lib():
         L.orc_scl_decode.argtypes = [i32, P, i32, P, i64, P, P, i32]
         L.orc_scl_decode_lazy.argtypes = [i32, P, i32, P, i64, P, P, i32]
         L.orc_polar_encode.argtypes = [i32, P, P, i64, P]
-        L.orc_scl_decode_mysn.argtypes = [i32, P, i32, P, i64, P, P, i32, i32, i32, ctypes.c_uint32, i32]
+        L.orc_scl_decode_mysn.argtypes = [i32, P, i32, P, i64, P, P, i32, i32, i32, ctypes.c_uint32, ctypes.c_double,
+                                          i32]
         L.orc_crc_encode.argtypes = [P, i64, i32, i32, ctypes.c_uint32, P]
         L.orc_crc_check.argtypes = [P, i64, i32, i32, ctypes.c_uint32, P]
         L.orc_np_pairwise_sum.argtypes = [P, i32]
@@ -134,8 +135,11 @@ def np_pairwise_sum(a):
     return lib().orc_np_pairwise_sum(_ptr(a), int(a.shape[0]))
 
 
-def scl_decode_mysn(llr_logits, frozen_pos, list_size=8, fast_scl=True, exact_f=True, crc=None, nthreads=0):
+def scl_decode_mysn(llr_logits, frozen_pos, list_size=8, fast_scl=True, exact_f=True, crc=None, nthreads=0,
+                    llr_max=30.0):
     """my_sn SCL_Dec.forward (dec.py:158-537): exact f, fast-SCL, optional CRC-aided pick.
+    llr_max: the decoder's clipping bound (self._llr_max, dec.py:213): f and metric clipping, the
+    dead-path metric (:420-422) and the CRC penalty llr_max*k (:517).
     Returns (bits float32 [bs,k], msg_pm float64 [bs,2L]: sorted, then CRC-penalised in place)."""
     x = np.ascontiguousarray(llr_logits, dtype=np.float32)
     bs, n = x.shape
@@ -145,7 +149,7 @@ def scl_decode_mysn(llr_logits, frozen_pos, list_size=8, fast_scl=True, exact_f=
     pm = np.empty((bs, 2 * list_size), dtype=np.float64)
     deg, g = crc_params(crc) if crc else (0, 0)
     r = lib().orc_scl_decode_mysn(n, _ptr(fm), int(list_size), _ptr(x), bs, _ptr(out), _ptr(pm), int(bool(fast_scl)),
-                                  int(bool(exact_f)), deg, g, int(nthreads))
+                                  int(bool(exact_f)), deg, g, float(llr_max), int(nthreads))
     if r < 0:
         raise ValueError("orc_scl_decode_mysn rejected its arguments")
     return out, pm

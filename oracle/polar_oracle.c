@@ -140,8 +140,8 @@ typedef struct {
 
 #define ROW(c, base, p, s) ((base) + ((size_t)(p) * ((c)->S + 1) + (s)) * (c)->n)
 
-static inline double f_minsum_d(double x, double y) {  /* polar_scl.py:93-106 (torch on f64) */
-    double xc = fmin(fmax(x, -30.0), 30.0), yc = fmin(fmax(y, -30.0), 30.0);
+static inline double f_minsum_d(double x, double y, double lmax) {  /* polar_scl.py:93-106 (torch on f64) */
+    double xc = fmin(fmax(x, -lmax), lmax), yc = fmin(fmax(y, -lmax), lmax);
     double sx = (double)((xc > 0) - (xc < 0)), sy = (double)((yc > 0) - (yc < 0));
     return sx * sy * fmin(fabs(xc), fabs(yc));
 }
@@ -162,7 +162,7 @@ static void scl_node(scl_ctx* c, int a, int s) {  /* polar_scl.py:121-177 */
         for (int p = 0; p < M; ++p) {
             double* in = ROW(c, c->llr, p, s);
             double* out = ROW(c, c->llr, p, s - 1);
-            for (int j = 0; j < h; ++j) out[a + j] = f_minsum_d(in[a + j], in[a + h + j]);
+            for (int j = 0; j < h; ++j) out[a + j] = f_minsum_d(in[a + j], in[a + h + j], 30.0);
         }
         scl_node(c, a, s - 1);
         for (int p = 0; p < M; ++p) {
@@ -261,6 +261,7 @@ typedef struct {
     uint8_t* beta;         /* [L][n] partial sums by absolute position */
     uint8_t* u;            /* [L][n] decided u */
     double pm[32];
+    double lmax;           /* clipping bound llr_max (reference: 30) */
     uint8_t* tmp_beta; uint8_t* tmp_u; int* tmp_sptr;
 } lz_ctx;
 
@@ -276,7 +277,7 @@ static void lz_node(lz_ctx* c, int a, int s) {
         for (int p = 0; p < L; ++p) {
             const double* in = lz_stage(c, p, s);
             double* out = c->alpha + (size_t)p * n + (1u << (s - 1));
-            for (int j = 0; j < h; ++j) out[j] = f_minsum_d(in[j], in[j + h]);
+            for (int j = 0; j < h; ++j) out[j] = f_minsum_d(in[j], in[j + h], c->lmax);
         }
         for (int p = 0; p < L; ++p) c->sptr[p * S1 + s - 1] = p;
         lz_node(c, a, s - 1);
@@ -296,7 +297,7 @@ static void lz_node(lz_ctx* c, int a, int s) {
         const int info = !c->frozen[a];
         double cand[64];
         for (int p = 0; p < L; ++p) {
-            const double l = fmax(fmin(lz_stage(c, p, 0)[0], 30.0), -30.0);
+            const double l = fmax(fmin(lz_stage(c, p, 0)[0], c->lmax), -c->lmax);
             cand[p] = c->pm[p] + log(1.0 + exp(-l));           /* u = 0 */
             cand[L + p] = c->pm[p] + log(1.0 + exp(-(-1.0 * l)));  /* u = 1 */
         }
@@ -340,7 +341,7 @@ int orc_scl_decode_lazy(int n, const uint8_t* frozen_mask, int L, const float* l
 #endif
     {
         lz_ctx c;
-        c.n = n; c.S = S; c.L = L; c.frozen = frozen_mask;
+        c.n = n; c.S = S; c.L = L; c.frozen = frozen_mask; c.lmax = 30.0;
         double* ch = (double*)malloc(sizeof(double) * (size_t)n);
         c.ch = ch;
         c.alpha = (double*)malloc(sizeof(double) * (size_t)L * n);
@@ -358,7 +359,7 @@ int orc_scl_decode_lazy(int n, const uint8_t* frozen_mask, int L, const float* l
             memset(c.beta, 0, (size_t)L * n);
             memset(c.u, 0, (size_t)L * n);
             for (int p = 0; p < L * (S + 1); ++p) c.sptr[p] = p / (S + 1);
-            for (int p = 0; p < L; ++p) c.pm[p] = p == 0 ? 0.0 : 30.0;
+            for (int p = 0; p < L; ++p) c.pm[p] = p == 0 ? 0.0 : c.lmax;
             lz_node(&c, 0, S);
             int best = 0;
             for (int p = 1; p < L; ++p) if (c.pm[p] < c.pm[best]) best = p;
@@ -445,8 +446,8 @@ int orc_crc_check(const float* in, int64_t bs, int len, int deg, uint32_t g, uin
     return 0;
 }
 
-static inline double f_exact_d(double x, double y) {  /* dec.py:330-339 on float64 */
-    const double xc = fmax(fmin(x, 30.0), -30.0), yc = fmax(fmin(y, 30.0), -30.0);
+static inline double f_exact_d(double x, double y, double lmax) {  /* dec.py:330-339 on float64 */
+    const double xc = fmax(fmin(x, lmax), -lmax), yc = fmax(fmin(y, lmax), -lmax);
     double o = log(1.0 + exp(xc + yc));
     o -= log(exp(xc) + exp(yc));
     return o;
@@ -491,7 +492,7 @@ static void my_node(my_ctx* mc, int a, int s) {
         if (nfz == len) {  /* rate-0 (dec.py:269-280): pm += sum softplus(-clip(llr)) */
             for (int p = 0; p < L; ++p) {
                 const double* in = lz_stage(c, p, s);
-                for (int j = 0; j < len; ++j) mc->terms[j] = log(1.0 + exp(-fmax(fmin(in[j], 30.0), -30.0)));
+                for (int j = 0; j < len; ++j) mc->terms[j] = log(1.0 + exp(-fmax(fmin(in[j], c->lmax), -c->lmax)));
                 c->pm[p] += orc_np_pairwise_sum(mc->terms, len);
                 memset(c->beta + (size_t)p * n + a, 0, (size_t)len);
             }
@@ -501,9 +502,9 @@ static void my_node(my_ctx* mc, int a, int s) {
             double cand[64];
             for (int p = 0; p < L; ++p) {
                 const double* in = lz_stage(c, p, s);
-                for (int j = 0; j < len; ++j) mc->terms[j] = log(1.0 + exp(-fmax(fmin(in[j], 30.0), -30.0)));
+                for (int j = 0; j < len; ++j) mc->terms[j] = log(1.0 + exp(-fmax(fmin(in[j], c->lmax), -c->lmax)));
                 cand[p] = c->pm[p] + orc_np_pairwise_sum(mc->terms, len);
-                for (int j = 0; j < len; ++j) mc->terms[j] = log(1.0 + exp(-fmax(fmin(-in[j], 30.0), -30.0)));
+                for (int j = 0; j < len; ++j) mc->terms[j] = log(1.0 + exp(-fmax(fmin(-in[j], c->lmax), -c->lmax)));
                 cand[L + p] = c->pm[p] + orc_np_pairwise_sum(mc->terms, len);
             }
             my_select(c, cand, a, len);
@@ -515,7 +516,7 @@ static void my_node(my_ctx* mc, int a, int s) {
         for (int p = 0; p < L; ++p) {
             const double* in = lz_stage(c, p, s);
             double* out = c->alpha + (size_t)p * n + (1u << (s - 1));
-            for (int j = 0; j < h; ++j) out[j] = mc->exact ? f_exact_d(in[j], in[j + h]) : f_minsum_d(in[j], in[j + h]);
+            for (int j = 0; j < h; ++j) out[j] = mc->exact ? f_exact_d(in[j], in[j + h], c->lmax) : f_minsum_d(in[j], in[j + h], c->lmax);
         }
         for (int p = 0; p < L; ++p) c->sptr[p * S1 + s - 1] = p;
         my_node(mc, a, s - 1);
@@ -536,7 +537,7 @@ static void my_node(my_ctx* mc, int a, int s) {
     /* leaf (dec.py:377-383): pm update every leaf; info leaves select and fork */
     double cand[64];
     for (int p = 0; p < L; ++p) {
-        const double l = fmax(fmin(lz_stage(c, p, 0)[0], 30.0), -30.0);
+        const double l = fmax(fmin(lz_stage(c, p, 0)[0], c->lmax), -c->lmax);
         cand[p] = c->pm[p] + log(1.0 + exp(-l));
         cand[L + p] = c->pm[p] + log(1.0 + exp(-(-1.0 * l)));
     }
@@ -550,7 +551,7 @@ static void my_node(my_ctx* mc, int a, int s) {
 /* SCL_Dec.forward of my_sn (dec.py:476-537).  crc_deg = 0: no CRC.  out_pm = msg_pm as the
  * reference leaves it: sorted by _decode_np_batch, then CRC-penalised in place, [bs][2L]. */
 int orc_scl_decode_mysn(int n, const uint8_t* frozen_mask, int L, const float* logits, int64_t bs, float* out_bits,
-                        double* out_pm, int fast_scl, int exact_f, int crc_deg, uint32_t crc_g, int nthreads) {
+                        double* out_pm, int fast_scl, int exact_f, int crc_deg, uint32_t crc_g, double llr_max, int nthreads) {
     const int S = ilog2(n);
     if (S < 0 || L < 1 || L > 32 || (L & (L - 1)) || !frozen_mask || !logits || !out_bits) return -1;
     int* info = (int*)malloc(sizeof(int) * (size_t)n);
@@ -565,7 +566,7 @@ int orc_scl_decode_mysn(int n, const uint8_t* frozen_mask, int L, const float* l
         my_ctx mc;
         lz_ctx* c = &mc.z;
         mc.fast = fast_scl; mc.exact = exact_f;
-        c->n = n; c->S = S; c->L = L; c->frozen = frozen_mask;
+        c->n = n; c->S = S; c->L = L; c->frozen = frozen_mask; c->lmax = llr_max;
         double* ch = (double*)malloc(sizeof(double) * (size_t)n);
         c->ch = ch;
         c->alpha = (double*)malloc(sizeof(double) * (size_t)L * n);
@@ -585,10 +586,10 @@ int orc_scl_decode_mysn(int n, const uint8_t* frozen_mask, int L, const float* l
             memset(c->beta, 0, (size_t)L * n);
             memset(c->u, 0, (size_t)L * n);
             for (int p = 0; p < L * (S + 1); ++p) c->sptr[p] = p / (S + 1);
-            for (int p = 0; p < L; ++p) c->pm[p] = p == 0 ? 0.0 : 30.0;
+            for (int p = 0; p < L; ++p) c->pm[p] = p == 0 ? 0.0 : c->lmax;
             my_node(&mc, 0, S);
             /* final sort (dec.py:202) of the 2L logical rows (row r < L = state r, row r >= L its
-             * copy), stable by pm; CRC penalty 30*k per failing row added in place (dec.py:515-518,
+             * copy), stable by pm; CRC penalty llr_max*k per failing row added in place (dec.py:515-518,
              * which also lands in the returned msg_pm: it aliases self.msg_pm); first argmin. */
             int row[64];
             for (int r = 0; r < 2 * L; ++r) row[r] = r;
@@ -607,7 +608,7 @@ int orc_scl_decode_mysn(int n, const uint8_t* frozen_mask, int L, const float* l
             double bestv = 0.0;
             for (int r = 0; r < 2 * L; ++r) {
                 const int p = row[r] % L;
-                const double v = c->pm[p] + (fail[p] ? 30.0 * (double)k : 0.0);
+                const double v = c->pm[p] + (fail[p] ? c->lmax * (double)k : 0.0);
                 if (out_pm) out_pm[b * 2 * L + r] = v;
                 if (r == 0 || v < bestv) { best = p; bestv = v; }
             }

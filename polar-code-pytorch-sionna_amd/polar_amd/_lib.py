@@ -33,6 +33,7 @@ def _declare(L):
     L.pl_plan_create.argtypes = [ctypes.POINTER(P), i32, P, i32, i32, ctypes.c_float, u32]
     L.pl_plan_destroy.argtypes = [P]
     L.pl_plan_info.argtypes = [P, P, P, P]
+    L.pl_plan_device.argtypes = [P, P]
     L.pl_sc_decode.argtypes = [P, P, i64, P, i32, P]
     L.pl_scl_workspace_size.argtypes = [P, i64]
     L.pl_scl_workspace_size.restype = ctypes.c_size_t
@@ -48,7 +49,7 @@ def _declare(L):
     L.pl_rate_recover.argtypes = [P, i64, i32, P, P, P, i32, P, P]
     L.pl_last_error_string.restype = ctypes.c_char_p
     L.pl_version.restype = ctypes.c_char_p
-    for f in (L.pl_plan_create, L.pl_plan_destroy, L.pl_plan_info, L.pl_sc_decode, L.pl_scl_decode,
+    for f in (L.pl_plan_create, L.pl_plan_destroy, L.pl_plan_info, L.pl_plan_device, L.pl_sc_decode, L.pl_scl_decode,
               L.pl_polar_encode, L.pl_plan_kernel, L.pl_sc_specialize, L.pl_sc_source, L.pl_plan_set_crc,
               L.pl_crc_attach,
               L.pl_gather_rows, L.pl_rate_recover):
@@ -70,7 +71,7 @@ def lib():
     return _lib
 
 
-EXPORTED_SYMBOLS = ("pl_plan_create", "pl_plan_destroy", "pl_plan_info", "pl_sc_decode",
+EXPORTED_SYMBOLS = ("pl_plan_create", "pl_plan_destroy", "pl_plan_info", "pl_plan_device", "pl_sc_decode",
                     "pl_scl_workspace_size", "pl_scl_decode", "pl_polar_encode",
                     "pl_plan_kernel", "pl_sc_specialize", "pl_sc_source", "pl_plan_set_crc", "pl_crc_attach",
                     "pl_gather_rows",
@@ -96,8 +97,34 @@ def current_stream_ptr(device):
 # the (512,1024) kernel and segfaults on at least one reference code.  So the Python layer
 # compiles with hipcc --genco in a child process (build.py ahead of time; Plan() for codes not
 # pre-built) and hands the library only cached code objects (PL_PLAN_CACHE_ONLY).
-HIPCC_GENCO = ["--offload-arch=gfx950", "--genco", "--no-gpu-bundle-output", "-O3", "-std=c++17",
-               "-ffp-contract=off"]
+#
+# The generated source starts with two lines written by the library (jit.cpp static_source):
+#   // pl-genco-flags: <hipcc flags>
+#   // pl-compiler: <__clang_version__ of the compiler that built libpolar_mi355x.so>
+# Both are part of the content-addressed cache name.  The flags are taken from there, and the
+# object is only built when `hipcc --version` reports that same compiler, so a cached object's
+# name always says which compiler and flags produced it.
+_GENCO_TAG, _COMPILER_TAG = "// pl-genco-flags: ", "// pl-compiler: "
+_hipcc_version = {}
+
+
+def _source_header(src):
+    flags = compiler = None
+    for line in src.splitlines()[:8]:
+        if line.startswith(_GENCO_TAG):
+            flags = line[len(_GENCO_TAG):].split()
+        elif line.startswith(_COMPILER_TAG):
+            compiler = line[len(_COMPILER_TAG):].strip()
+    return flags, compiler
+
+
+def hipcc_version(hipcc):
+    """`hipcc --version` text (cached per path)."""
+    import subprocess
+    if hipcc not in _hipcc_version:
+        r = subprocess.run([hipcc, "--version"], capture_output=True, text=True, timeout=120)
+        _hipcc_version[hipcc] = r.stdout if r.returncode == 0 else ""
+    return _hipcc_version[hipcc]
 
 
 def sc_source(n, frozen_mask_u8, f_mode):
@@ -134,11 +161,21 @@ def hipcc_path():
 
 
 def compile_code_object(src, out_dir, name, timeout=600):
-    """hipcc --genco of one specialised kernel into out_dir/name (atomic rename).  True on success."""
+    """hipcc --genco of one specialised kernel into out_dir/name (atomic rename).  True on success;
+    False when hipcc is missing, is not the compiler named in the source, or fails."""
+    import shutil
     import subprocess
     import tempfile
     hipcc = hipcc_path()
     if hipcc is None:
+        return False
+    flags, compiler = _source_header(src)
+    if not flags or not compiler:
+        raise ValueError("specialised SC source without its build header (pl-genco-flags / pl-compiler)")
+    if compiler not in hipcc_version(hipcc):
+        import warnings
+        warnings.warn(f"{hipcc} is not the compiler libpolar_mi355x.so was built with ({compiler}); rebuild the "
+                      "library (python -m polar_amd.build) to compile specialised SC kernels")
         return False
     os.makedirs(out_dir, exist_ok=True)
     with tempfile.TemporaryDirectory(prefix="pl_sc_") as td:
@@ -146,11 +183,10 @@ def compile_code_object(src, out_dir, name, timeout=600):
         with open(hip, "w") as f:
             f.write(src)
         tmp = os.path.join(td, name)
-        r = subprocess.run([hipcc, *HIPCC_GENCO, hip, "-o", tmp], capture_output=True, text=True, timeout=timeout)
+        r = subprocess.run([hipcc, *flags, hip, "-o", tmp], capture_output=True, text=True, timeout=timeout)
         if r.returncode != 0 or not os.path.exists(tmp):
             return False
         part = os.path.join(out_dir, f".{name}.{os.getpid()}.part")
-        import shutil
         shutil.copyfile(tmp, part)
         os.replace(part, os.path.join(out_dir, name))
     return True
@@ -175,12 +211,32 @@ def ensure_sc_kernel(n, frozen_mask_u8, f_mode):
     return False
 
 
-class Plan:
-    """Owning wrapper of a pl_plan* (immutable, usable from any stream)."""
+def device_index(device=None):
+    """CUDA device index of `device` (None: the current device; None without a visible GPU)."""
+    if device is None:
+        return torch.cuda.current_device() if torch.cuda.is_available() else None
+    if isinstance(device, int):
+        return device
+    d = torch.device(device)
+    if d.type != "cuda":
+        raise ValueError(f"plans live on a ROCm GPU, not on {d}")
+    return d.index if d.index is not None else torch.cuda.current_device()
 
-    def __init__(self, n, frozen_mask_u8, list_size=1, f_mode=PL_F_MINSUM, llr_max=30.0, flags=0):
-        """flags: 0 (SC plans get a kernel specialised to the frozen set), PL_PLAN_GENERIC or
-        PL_PLAN_CACHE_ONLY (see include/polar_mi355x.h)."""
+
+class Plan:
+    """Owning wrapper of a pl_plan* (immutable, usable from any stream of its device).
+
+    A plan is device-bound: pl_plan_create allocates its tables and loads its specialised kernel
+    on the current device, so the plan is created inside `torch.cuda.device(device)` and the
+    library rejects launches on another device's stream (PL_EINVAL).  Use PlanSet for one plan
+    per device."""
+
+    def __init__(self, n, frozen_mask_u8, list_size=1, f_mode=PL_F_MINSUM, llr_max=30.0, flags=0, device=None):
+        """flags: 0 (SC plans get a kernel specialised to the frozen set), PL_PLAN_GENERIC,
+        PL_PLAN_CACHE_ONLY or PL_PLAN_FAST_SCL (see include/polar_mi355x.h).  device: the GPU the
+        plan lives on (default: the current device)."""
+        import contextlib
+
         import numpy as np
         mask = np.ascontiguousarray(frozen_mask_u8, dtype=np.uint8)
         assert mask.shape == (n,)
@@ -189,12 +245,16 @@ class Plan:
             # the library only loads cached code objects; compile out of process when missing
             ensure_sc_kernel(n, mask, f_mode)
             flags |= PL_PLAN_CACHE_ONLY
+        idx = device_index(device)
         self._h = ctypes.c_void_p()
-        check(lib().pl_plan_create(ctypes.byref(self._h), int(n), mask.ctypes.data_as(ctypes.c_void_p),
-                                   int(list_size), int(f_mode), float(llr_max), int(flags)), "pl_plan_create")
-        n_, k_, l_ = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
+        with (torch.cuda.device(idx) if idx is not None else contextlib.nullcontext()):
+            check(lib().pl_plan_create(ctypes.byref(self._h), int(n), mask.ctypes.data_as(ctypes.c_void_p),
+                                       int(list_size), int(f_mode), float(llr_max), int(flags)), "pl_plan_create")
+        n_, k_, l_, d_ = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int32()
         check(lib().pl_plan_info(self._h, ctypes.byref(n_), ctypes.byref(k_), ctypes.byref(l_)), "pl_plan_info")
+        check(lib().pl_plan_device(self._h, ctypes.byref(d_)), "pl_plan_device")
         self.n, self.k, self.list_size = n_.value, k_.value, l_.value
+        self.device = torch.device("cuda", d_.value)
 
     @property
     def handle(self):
@@ -213,8 +273,48 @@ class Plan:
                  PL_KERNEL_SCL_SUBTREE: "scl_subtree"}
         return names[kind.value], buf.value.decode()
 
+    def __deepcopy__(self, memo):  # a copy would double-free the handle
+        raise TypeError("polar_amd Plan objects are not copyable; build another Plan")
+
+    def __reduce__(self):
+        raise TypeError("polar_amd Plan objects are not picklable")
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and h.value and _lib is not None:
             _lib.pl_plan_destroy(h)
             self._h = None
+
+
+class PlanSet:
+    """The plans of one code, one per GPU, made on first use by `make(device_index)`.
+
+    Decoder modules keep one of these instead of a single plan, so a module works on whichever
+    device its input is on (and replicas of a module on several GPUs share it).  Copying or
+    pickling a module gives it an empty set (plans are rebuilt on first use)."""
+
+    def __init__(self):
+        self._plans = {}
+        self._lock = threading.Lock()
+
+    def get(self, device, make):
+        idx = device_index(device)
+        p = self._plans.get(idx)
+        if p is None:
+            with self._lock:
+                p = self._plans.get(idx)
+                if p is None:
+                    p = self._plans[idx] = make(idx)
+        return p
+
+    def __len__(self):
+        return len(self._plans)
+
+    def __deepcopy__(self, memo):
+        return PlanSet()
+
+    def __getstate__(self):
+        return {}
+
+    def __setstate__(self, state):
+        self.__init__()

@@ -148,11 +148,16 @@ class GpuEncoder(nn.Module):
         super().__init__()
         from . import _lib
         from .frozen import frozen_mask
-        self._plan = _lib.Plan(n, frozen_mask(frozen_pos, n), 1)
+        self._n, self._mask = n, frozen_mask(frozen_pos, n)
+        self._plans = _lib.PlanSet()
+
+    def _make_plan(self, dev):
+        from . import _lib
+        return _lib.Plan(self._n, self._mask, 1, flags=_lib.PL_PLAN_GENERIC, device=dev)
 
     def forward(self, u):
         from . import ops
-        return ops.polar_encode(self._plan, u)
+        return ops.polar_encode(self._plans.get(u.device, self._make_plan), u)
 
 
 class System_AWGN_model(nn.Module):

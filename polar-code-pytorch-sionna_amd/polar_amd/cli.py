@@ -87,10 +87,13 @@ def main(argv=None):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     pg = None
+    if tc.cuda.is_available():
+        # one GPU per rank whichever backend carries the counters: the decoders run on the
+        # current device when the LLRs are produced on the CPU (gloo path)
+        tc.cuda.set_device(local % tc.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
         if c.llr_device == "cuda":
-            tc.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=tc.device("cuda", local))
         else:
             dist.init_process_group("gloo")

@@ -28,6 +28,20 @@ int check_hip(hipError_t e, const char* what) {
     set_error(std::string(what) + ": " + hipGetErrorString(e));
     return PL_EHIP;
 }
+// A plan's tables (hipMalloc) and specialised kernel module (hipModuleLoadData) belong to the
+// device that was current at pl_plan_create; launching it on another device's stream would hand
+// that device foreign pointers and a foreign module.
+int check_device(const pl_plan* p, hipStream_t st, const char* what) {
+    int dev = -1;
+    const hipError_t e = st ? hipStreamGetDevice(st, &dev) : hipGetDevice(&dev);
+    if (e != hipSuccess) return check_hip(e, what);
+    if (dev != p->device) {
+        set_error(std::string(what) + ": the plan was created on device " + std::to_string(p->device) +
+                  " but the stream is on device " + std::to_string(dev) + " (plans are device-bound)");
+        return PL_EINVAL;
+    }
+    return PL_OK;
+}
 }  // namespace pl
 
 namespace {
@@ -48,6 +62,10 @@ int upload(T** dst, const std::vector<T>& src) {
 
 void free_plan(pl_plan* p) {
     if (!p) return;
+    // release on the plan's own device (the module and the tables live there)
+    int cur = -1;
+    const bool switch_dev = hipGetDevice(&cur) == hipSuccess && p->device >= 0 && cur != p->device &&
+                            hipSetDevice(p->device) == hipSuccess;
     pl::detach_static(p);
     (void)hipFree(p->d_info_loc);
     (void)hipFree(p->d_frozen_words);
@@ -55,6 +73,7 @@ void free_plan(pl_plan* p) {
     (void)hipFree(p->d_type_words);
     (void)hipFree(p->d_info_pos);
     (void)hipFree(p->d_info_rank);
+    if (switch_dev) (void)hipSetDevice(cur);
     delete p;
 }
 
@@ -63,7 +82,7 @@ void free_plan(pl_plan* p) {
 extern "C" {
 
 const char* pl_last_error_string(void) { return g_last_error.c_str(); }
-const char* pl_version(void) { return "polar_mi355x 0.1.0 (gfx950)"; }
+const char* pl_version(void) { return "polar_mi355x 0.2.0 (gfx950)"; }
 
 int pl_plan_create(pl_plan** out, int32_t n, const uint8_t* frozen_mask, int32_t list_size, int32_t f_mode,
                    float llr_max, uint32_t flags) {
@@ -98,6 +117,14 @@ int pl_plan_create(pl_plan** out, int32_t n, const uint8_t* frozen_mask, int32_t
     p->f_mode = f_mode;
     p->llr_max = llr_max;
     p->flags = flags;
+    if (list_size > 1 && !pl::scl_supported(p)) {  // reject at construction, not at the first decode
+        delete p;
+        return PL_ENOTSUP;
+    }
+    if (int r = pl::check_hip(hipGetDevice(&p->device), "pl_plan_create: hipGetDevice")) {
+        delete p;
+        return r;
+    }
 
     const int nwords = (n + 31) / 32;
     std::vector<uint32_t> fw(nwords, 0u);
@@ -181,6 +208,15 @@ int pl_plan_set_crc(pl_plan* p, int32_t degree, uint32_t poly_mask) {
     return PL_OK;
 }
 
+int pl_plan_device(const pl_plan* p, int32_t* device) {
+    if (!p || !device) {
+        pl::set_error("pl_plan_device: null argument");
+        return PL_EINVAL;
+    }
+    *device = p->device;
+    return PL_OK;
+}
+
 int pl_plan_info(const pl_plan* p, int32_t* n, int32_t* k, int32_t* list_size) {
     if (!p) {
         pl::set_error("pl_plan_info: null plan");
@@ -201,6 +237,7 @@ int pl_sc_decode(const pl_plan* p, const float* llr, int64_t bs, void* out, int3
         pl::set_error("pl_sc_decode: unknown out_kind");
         return PL_EINVAL;
     }
+    if (int r = pl::check_device(p, static_cast<hipStream_t>(stream), "pl_sc_decode")) return r;
     if (p->sc_module) return pl::launch_sc_static(p, llr, bs, out, out_kind, static_cast<hipStream_t>(stream));
     return pl::launch_sc(p, llr, bs, out, out_kind, static_cast<hipStream_t>(stream));
 }
@@ -221,6 +258,7 @@ int pl_scl_decode(const pl_plan* p, const float* llr, int64_t bs, void* out, int
         pl::set_error("pl_scl_decode: workspace too small");
         return PL_EINVAL;
     }
+    if (int r = pl::check_device(p, static_cast<hipStream_t>(stream), "pl_scl_decode")) return r;
     return pl::launch_scl(p, llr, bs, out, out_kind, out_pm, ws, ws_bytes, static_cast<hipStream_t>(stream));
 }
 
@@ -229,6 +267,7 @@ int pl_polar_encode(const pl_plan* p, const float* u, int64_t bs, float* cw, voi
         pl::set_error("pl_polar_encode: bad arguments");
         return PL_EINVAL;
     }
+    if (int r = pl::check_device(p, static_cast<hipStream_t>(stream), "pl_polar_encode")) return r;
     return pl::launch_encode(p, u, bs, cw, static_cast<hipStream_t>(stream));
 }
 

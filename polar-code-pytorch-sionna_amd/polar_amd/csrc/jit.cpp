@@ -37,6 +37,13 @@ const char kStaticSrc[] =
 const char* kOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off"};
 constexpr int kNumOpts = sizeof(kOpts) / sizeof(kOpts[0]);
 
+// Out-of-process build of a specialised kernel (polar_amd/_lib.py compile_code_object reads both
+// lines from the head of the generated source): the hipcc flags, and the compiler this library
+// was built with.  Both are part of the source, hence of the cache name, so a code object built
+// with other flags or by another compiler release is never picked up under this name; the Python
+// side refuses to compile when `hipcc --version` does not report the same compiler.
+const char kGencoFlags[] = "--offload-arch=gfx950 --genco --no-gpu-bundle-output -O3 -std=c++17 -ffp-contract=off";
+
 enum : int { R0 = 0, R1 = 1, REP = 2, SPC = 3, GEN = 4 };
 
 uint64_t fnv1a(const std::string& s, uint64_t h = 1469598103934665603ull) {
@@ -161,6 +168,7 @@ std::string static_source(int n, const uint8_t* frozen, int f_mode) {
             }
     }
     std::ostringstream o;
+    o << "// pl-genco-flags: " << kGencoFlags << "\n// pl-compiler: " << __clang_version__ << "\n";
     if (tuned_wide(log_n, f_mode)) o << "#define PL_SC_MINW 3\n#define PL_SC_F_BITOP3 1\n";
     // PL_SC_DEFINES="NAME=VALUE ..." overrides the kernel's tuning macros (development variants;
     // part of the source, hence of the cache key)
@@ -186,13 +194,22 @@ std::string static_source(int n, const uint8_t* frozen, int f_mode) {
     return o.str();
 }
 
+// Cache file names.  hipcc --genco objects ("sc_"): the source names flags and compiler (above).
+// In-process hiprtc objects ("scr_"): the source plus the hiprtc options and version -- a
+// different compiler build, so never shared with the hipcc name.
 std::string cache_name(const std::string& src) {
+    char buf[32];
+    snprintf(buf, sizeof buf, "sc_%016llx.co", (unsigned long long)fnv1a(src));
+    return buf;
+}
+
+std::string cache_name_hiprtc(const std::string& src) {
     std::string key = src;
     for (int i = 0; i < kNumOpts; ++i) key += std::string("\n//opt ") + kOpts[i];
     int major = 0, minor = 0;
     if (hiprtcVersion(&major, &minor) == HIPRTC_SUCCESS) key += "\n//hiprtc " + std::to_string(major) + "." + std::to_string(minor);
     char buf[32];
-    snprintf(buf, sizeof buf, "sc_%016llx.co", (unsigned long long)fnv1a(key));
+    snprintf(buf, sizeof buf, "scr_%016llx.co", (unsigned long long)fnv1a(key));
     return buf;
 }
 
@@ -200,14 +217,16 @@ std::string cache_name(const std::string& src) {
 int specialize(int n, const uint8_t* frozen, int f_mode, const char* forced_dir, bool allow_compile,
                std::vector<char>& image, std::string& path) {
     const std::string src = static_source(n, frozen, f_mode);
-    const std::string name = cache_name(src);
+    const std::string name = cache_name_hiprtc(src);
     std::vector<std::string> dirs;
     if (forced_dir && *forced_dir) dirs.push_back(forced_dir);
     else dirs = cache_dirs();
-    for (const auto& d : dirs) {
-        if (read_file(d + "/" + name, image)) {
-            path = d + "/" + name;
-            return PL_OK;
+    for (const std::string& nm : {cache_name(src), name}) {  // hipcc-built first
+        for (const auto& d : dirs) {
+            if (read_file(d + "/" + nm, image)) {
+                path = d + "/" + nm;
+                return PL_OK;
+            }
         }
     }
     if (!allow_compile) {

@@ -9,6 +9,7 @@ struct pl_plan {
     int32_t n = 0, log_n = 0, k = 0, list_size = 1, f_mode = 0;
     float llr_max = 30.0f;
     uint32_t flags = 0;
+    int32_t device = -1;                 // HIP device the plan's tables and module live on
     // Device-resident, immutable after pl_plan_create:
     uint32_t* d_frozen_words = nullptr;  // ceil(n/32) words, bit (i&31) of word i>>5 = frozen[i]
     uint32_t* d_rate0_words = nullptr;   // n-1 node flags: bit OFF(s)+(p>>s), OFF(s)=n-(n>>(s-1))
@@ -39,8 +40,12 @@ int launch_scl(const pl_plan* plan, const float* llr, int64_t bs, void* out, int
                double* out_pm, void* ws, size_t ws_bytes, hipStream_t stream);
 // SCL "register subtree" kernel (scl_tree_kernel.hip); launch_scl dispatches to it when eligible
 bool scl_tree_eligible(const pl_plan* plan);
+// Whether some SCL kernel decodes this plan (sets the error string when not); scl_kernel.hip
+bool scl_supported(const pl_plan* plan);
 int launch_scl_tree(const pl_plan* plan, const float* llr, int64_t bs, void* out, int out_kind, double* out_pm,
                     hipStream_t stream);
+// PL_OK when the stream (NULL: the current device) is on the plan's device, else PL_EINVAL; capi.cpp
+int check_device(const pl_plan* plan, hipStream_t stream, const char* what);
 int launch_encode(const pl_plan* plan, const float* u, int64_t bs, float* cw, hipStream_t stream);
 
 // Code-specialised SC kernels (jit.cpp)

@@ -27,7 +27,7 @@
 //             log(1+exp(-clip(llr))) over the node (:269-280); a repetition node forks once on
 //             the two node sums (:281-306).  Sums follow numpy's pairwise order (np.sum over the
 //             last axis) so path metrics match to rounding.
-//   CRC       CRC-aided pick (:507-518): every path failing the CRC gets +30*k, first argmin; the
+//   CRC       CRC-aided pick (:507-518): every path failing the CRC gets +llr_max*k, first argmin; the
 //             penalty also lands in the returned metrics (it aliases msg_pm in the reference).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -35,6 +35,8 @@
 #include "../../../include/polar_mi355x.h"
 #include "plan.h"
 #include "softplus.h"
+
+#include <string>
 
 namespace {
 
@@ -52,7 +54,10 @@ __host__ __device__ inline Lay make_layout(int n, int log_n, int L) {
     y.L = L;
     y.W = n >= 32 ? n / 32 : 1;
     int o = 0;
-    y.off_alpha = o; o = align16(o + L * (n / 2 > 0 ? n / 2 : 1) * 8);
+    // L stage regions of n/2 doubles; at least n doubles, the staging area of the node terms of a
+    // pruned root (node_softplus_sums, one path at a time)
+    const int na = L * (n / 2 > 0 ? n / 2 : 1);
+    y.off_alpha = o; o = align16(o + (na > n ? na : n) * 8);
     y.off_ch = o; o = align16(o + n * 4);
     y.off_beta = o; o = align16(o + L * y.W * 4);
     y.off_u = o; o = align16(o + L * y.W * 4);
@@ -452,7 +457,7 @@ __global__ __launch_bounds__(64) void scl_decode_kernel(const float* __restrict_
         double bestv = 0.0;
         for (int r = 0; r < 2 * L; ++r) {
             const int p = row[r] % L;
-            const double v = t.pm[p] + (fail_s[p] ? 30.0 * (double)k : 0.0);
+            const double v = t.pm[p] + (fail_s[p] ? t.lmax * (double)k : 0.0);
             if (out_pm != nullptr && lane == 0) out_pm[b * 2 * L + r] = v;
             if (r == 0 || v < bestv) {
                 best = p;
@@ -474,19 +479,28 @@ __global__ __launch_bounds__(64) void scl_decode_kernel(const float* __restrict_
 namespace pl {
 size_t scl_workspace_size(const pl_plan*, int64_t) { return 0; }
 
+// Limits of the generic kernel: its state is LDS-resident (one wave per codeword, <= 160 KiB)
+// and a fork gathers the L * n/32 partial-sum and decision words in 16 registers per lane
+// (select_fork: R = 16), and the L * log n stage owners in 8 (RS = 8).  At n = 2048 that is
+// L <= 16 (147.6 KB of LDS at L = 16).  The subtree kernel covers 2 <= L <= 32 up to n = 1024.
+bool scl_supported(const pl_plan* p) {
+    if (scl_tree_eligible(p)) return true;
+    const int L = p->list_size, W = p->n >= 32 ? p->n / 32 : 1;
+    const Lay y = make_layout(p->n, p->log_n, L);
+    if (L * W > 16 * 64 || L * p->log_n > 8 * 64 || y.bytes > 160 * 1024) {
+        set_error("SCL decode: n = " + std::to_string(p->n) + " with list_size " + std::to_string(L) +
+                  " is not supported (the list state must fit one CU's LDS: list_size <= 16 at n = 2048)");
+        return false;
+    }
+    return true;
+}
+
 int launch_scl(const pl_plan* p, const float* llr, int64_t bs, void* out, int out_kind, double* out_pm, void*, size_t,
                hipStream_t st) {
     if (bs == 0) return PL_OK;
     if (scl_tree_eligible(p)) return launch_scl_tree(p, llr, bs, out, out_kind, out_pm, st);
-    if (p->n > 1024) {
-        set_error("SCL decode: n must be <= 1024");
-        return PL_ENOTSUP;
-    }
+    if (!scl_supported(p)) return PL_ENOTSUP;
     const Lay y = make_layout(p->n, p->log_n, p->list_size);
-    if (y.bytes > 160 * 1024) {
-        set_error("SCL decode: n * list_size too large for LDS");
-        return PL_ENOTSUP;
-    }
     const bool fast = (p->flags & PL_PLAN_FAST_SCL) != 0;
     const bool exact = p->f_mode == PL_F_EXACT;
     const void* fn = nullptr;

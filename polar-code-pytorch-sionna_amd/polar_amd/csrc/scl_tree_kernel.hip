@@ -1140,7 +1140,7 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
             const double v = mine.pm_s[c & (L - 1)];
             rk += (v < mv || (v == mv && c < gl)) ? 1 : 0;
         }
-        const double val = mv + (mine.fail_s[p] ? 30.0 * (double)k : 0.0);
+        const double val = mv + (mine.fail_s[p] ? t.lmax * (double)k : 0.0);
         mine.sv[rk] = val;
         mine.sp[rk] = p;
         if (out_pm != nullptr && t.b0 + my_c < bs) out_pm[(t.b0 + my_c) * GW + rk] = val;

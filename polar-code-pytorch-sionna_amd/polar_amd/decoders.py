@@ -22,6 +22,16 @@ def _frozen_mask(frozen_pos, n):
     return fp, m
 
 
+def check_supported(n, list_size=1):
+    """Raise ValueError at construction for codes no MI355X kernel decodes (the C library's
+    limits, include/polar_mi355x.h: n <= 2048; list decoding at n = 2048 needs list_size <= 16)."""
+    n, list_size = int(n), int(list_size)
+    if n > 2048 or (list_size > 1 and n > 1024 and list_size > 16):
+        what = "SC" if list_size == 1 else f"SCL (list_size {list_size})"
+        raise ValueError(f"{what} decoding of n = {n} is not supported by the MI355X kernels "
+                         "(n <= 2048; list_size <= 16 at n = 2048)")
+
+
 def _gpu_for(inputs, module_device):
     if inputs.device.type == "cuda":
         return inputs.device
@@ -51,12 +61,15 @@ class SC_Dec(nn.Module):
         self.device = device
         self._n_stages = int(np.log2(n))
         self._mask = mask
-        self._plan = None
+        check_supported(n)
+        self._plans = _lib.PlanSet()
 
-    def plan(self):
-        if self._plan is None:
-            self._plan = _lib.Plan(self.n, self._mask, 1, _lib.PL_F_MINSUM, self.llr_max)
-        return self._plan
+    def plan(self, device=None):
+        """The decoding plan on `device` (default: the current GPU); plans are device-bound."""
+        return self._plans.get(device, self._make_plan)
+
+    def _make_plan(self, dev):
+        return _lib.Plan(self.n, self._mask, 1, _lib.PL_F_MINSUM, self.llr_max, device=dev)
 
     def forward(self, inputs):
         if self.mode not in ("llr", "max"):  # polar_sc.py:44-45 raises inside f
@@ -67,7 +80,7 @@ class SC_Dec(nn.Module):
         input_shape = inputs.shape
         llr = inputs.reshape([-1, self.n])
         dev = _gpu_for(llr, self.device)
-        u_hat = ops.sc_decode(self.plan(), llr.to(dev, non_blocking=True))
+        u_hat = ops.sc_decode(self.plan(dev), llr.to(dev, non_blocking=True))
         output_shape = list(input_shape)
         output_shape[-1] = self.k
         output_shape[0] = -1
@@ -104,7 +117,8 @@ class SCL_Dec(nn.Module):
         self._frozen_ind = mask.astype(np.float64)
         self._n_stages = int(np.log2(self._n))
         self._mask = mask
-        self._plan = None
+        check_supported(n, list_size)
+        self._plans = _lib.PlanSet()
         self._pm = None
 
     @property
@@ -123,10 +137,12 @@ class SCL_Dec(nn.Module):
     def msg_pm(self):
         return None if self._pm is None else self._pm.cpu().numpy()
 
-    def plan(self):
-        if self._plan is None:
-            self._plan = _lib.Plan(self._n, self._mask, self._list_size, _lib.PL_F_MINSUM, self._llr_max)
-        return self._plan
+    def plan(self, device=None):
+        """The decoding plan on `device` (default: the current GPU); plans are device-bound."""
+        return self._plans.get(device, self._make_plan)
+
+    def _make_plan(self, dev):
+        return _lib.Plan(self._n, self._mask, self._list_size, _lib.PL_F_MINSUM, self._llr_max, device=dev)
 
     def forward(self, inputs):
         assert inputs.dtype == self.output_dtype, "Invalid input dtype."
@@ -136,7 +152,7 @@ class SCL_Dec(nn.Module):
         input_shape = inputs.shape
         llr = inputs.reshape([-1, self._n])
         dev = _gpu_for(llr, self.device)
-        u_hat, self._pm = ops.scl_decode(self.plan(), llr.to(dev, non_blocking=True), return_pm=True)
+        u_hat, self._pm = ops.scl_decode(self.plan(dev), llr.to(dev, non_blocking=True), return_pm=True)
         output_shape = list(input_shape)
         output_shape[-1] = self.k
         output_shape[0] = -1

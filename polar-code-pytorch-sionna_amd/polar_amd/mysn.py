@@ -5,8 +5,9 @@
                (use_fast_scl, :367-376), optional CRC-aided pick (crc_degree, :507-518)
 
 Both run in libpolar_mi355x.so on a ROCm GPU (SC: the per-code specialised kernel in exact-f mode;
-SCL: the subtree kernel scl_tree_kernel.hip with exact f / fast-SCL / CRC, the generic
-scl_kernel.hip for n > 1024).  Differences from the reference are stated where
+SCL: the subtree kernel scl_tree_kernel.hip with exact f / fast-SCL / CRC for 32 <= n <= 1024,
+the generic scl_kernel.hip otherwise -- n = 2048 with list_size <= 16, the largest list state
+that fits one CU's LDS; larger codes raise ValueError at construction).  Differences from the reference are stated where
 they exist:
   * The reference's CRCEncoder cannot be constructed as shipped (crc.py:81 reads self.device,
     which is never set), so SCL_Dec(crc_degree=...) raises there; here it works, with the CRC of
@@ -21,7 +22,7 @@ import torch as tc
 from torch import nn
 
 from . import _lib, ops
-from .decoders import _frozen_mask, _gpu_for
+from .decoders import _frozen_mask, _gpu_for, check_supported
 
 # 5G CRC polynomials (my_sn/fec/crc.py:38-52 / 3GPP TS 38.212 Sec. 5.1), exponents
 CRC_POLYS = {"CRC24A": [24, 23, 18, 17, 14, 11, 10, 7, 6, 5, 4, 3, 1, 0], "CRC24B": [24, 23, 6, 5, 1, 0],
@@ -54,12 +55,15 @@ class SC_Dec(nn.Module):
         self._use_fast_sc = False
         self.device = device
         self._mask = mask
-        self._plan = None
+        check_supported(n)
+        self._plans = _lib.PlanSet()
 
-    def plan(self):
-        if self._plan is None:
-            self._plan = _lib.Plan(self.n, self._mask, 1, _lib.PL_F_EXACT, self.llr_max)
-        return self._plan
+    def plan(self, device=None):
+        """The decoding plan on `device` (default: the current GPU); plans are device-bound."""
+        return self._plans.get(device, self._make_plan)
+
+    def _make_plan(self, dev):
+        return _lib.Plan(self.n, self._mask, 1, _lib.PL_F_EXACT, self.llr_max, device=dev)
 
     def forward(self, inputs):
         inputs = inputs.to(dtype=tc.float32)
@@ -68,7 +72,7 @@ class SC_Dec(nn.Module):
         input_shape = inputs.shape
         llr = inputs.reshape([-1, self.n])
         dev = _gpu_for(llr, self.device)
-        u_hat = ops.sc_decode(self.plan(), llr.to(dev, non_blocking=True))
+        u_hat = ops.sc_decode(self.plan(dev), llr.to(dev, non_blocking=True))
         output_shape = list(input_shape)
         output_shape[-1] = self.k
         output_shape[0] = -1
@@ -121,7 +125,8 @@ class SCL_Dec(nn.Module):
         if use_hybrid_sc:
             raise NotImplementedError("use_hybrid_sc: not implemented in the reference either (dec.py:497-498)")
         self._mask = mask
-        self._plan = None
+        check_supported(n, list_size)
+        self._plans = _lib.PlanSet()
         self._pm = None
 
     @property
@@ -156,14 +161,16 @@ class SCL_Dec(nn.Module):
     def msg_pm(self):
         return None if self._pm is None else self._pm.cpu().numpy()
 
-    def plan(self):
-        if self._plan is None:
-            flags = _lib.PL_PLAN_FAST_SCL if self._use_fast_scl else 0
-            p = _lib.Plan(self._n, self._mask, self._list_size, _lib.PL_F_EXACT, self._llr_max, flags=flags)
-            if self._use_crc:
-                p.set_crc(*self._crc)
-            self._plan = p
-        return self._plan
+    def plan(self, device=None):
+        """The decoding plan on `device` (default: the current GPU); plans are device-bound."""
+        return self._plans.get(device, self._make_plan)
+
+    def _make_plan(self, dev):
+        flags = _lib.PL_PLAN_FAST_SCL if self._use_fast_scl else 0
+        p = _lib.Plan(self._n, self._mask, self._list_size, _lib.PL_F_EXACT, self._llr_max, flags=flags, device=dev)
+        if self._use_crc:
+            p.set_crc(*self._crc)
+        return p
 
     def forward(self, inputs):
         assert inputs.dtype == self.output_dtype, "Invalid input dtype."
@@ -175,7 +182,7 @@ class SCL_Dec(nn.Module):
         input_shape = inputs.shape
         llr = inputs.reshape([-1, self._n])
         dev = _gpu_for(llr, self.device)
-        u_hat, self._pm = ops.scl_decode(self.plan(), llr.to(dev, non_blocking=True), return_pm=True)
+        u_hat, self._pm = ops.scl_decode(self.plan(dev), llr.to(dev, non_blocking=True), return_pm=True)
         output_shape = list(input_shape)
         output_shape[-1] = self.k
         output_shape[0] = -1

@@ -45,8 +45,15 @@ def sc_decode(plan, llr_logits, out=None, out_dtype=torch.float32):
     return out
 
 
-def scl_decode(plan, llr_logits, out=None, out_dtype=torch.float32, return_pm=False):
-    """SCL-decode [bs, n] fp32 logits -> [bs, k] bits (+ sorted path metrics [bs, 2L] fp64)."""
+def scl_workspace(plan, bs, device):
+    """A device workspace of pl_scl_workspace_size(plan, bs) bytes (reusable across calls)."""
+    ws_bytes = int(_lib.lib().pl_scl_workspace_size(plan.handle, bs))
+    return torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=device)
+
+
+def scl_decode(plan, llr_logits, out=None, out_dtype=torch.float32, return_pm=False, workspace=None):
+    """SCL-decode [bs, n] fp32 logits -> [bs, k] bits (+ sorted path metrics [bs, 2L] fp64).
+    workspace: optional uint8 device tensor from scl_workspace() (allocated per call if None)."""
     _require_cuda(llr_logits, "llr_logits")
     x = llr_logits
     if x.dtype != torch.float32 or not x.is_contiguous():
@@ -60,7 +67,9 @@ def scl_decode(plan, llr_logits, out=None, out_dtype=torch.float32, return_pm=Fa
     pm = torch.empty((bs, 2 * plan.list_size), dtype=torch.float64, device=x.device) if return_pm else None
     L = _lib.lib()
     ws_bytes = int(L.pl_scl_workspace_size(plan.handle, bs))
-    ws = torch.empty((max(ws_bytes, 1),), dtype=torch.uint8, device=x.device)
+    ws = workspace if workspace is not None else scl_workspace(plan, bs, x.device)
+    if ws.device != x.device or ws.numel() < ws_bytes:
+        raise ValueError(f"workspace must hold {ws_bytes} bytes on {x.device}")
     with torch.cuda.device(x.device):
         st = _lib.current_stream_ptr(x.device)
         _lib.check(L.pl_scl_decode(plan.handle, ctypes.c_void_p(x.data_ptr()), bs, ctypes.c_void_p(out.data_ptr()),

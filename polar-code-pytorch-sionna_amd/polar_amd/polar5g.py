@@ -221,7 +221,7 @@ class PolarEncoder(nn.Module):
         assert self._k == len(self.info_pos), "Internal error: invalid info_pos generated."
         self._mask = np.zeros(n, dtype=np.uint8)
         self._mask[frozen_pos.astype(np.int64)] = 1
-        self._plan = None
+        self._plans = _lib.PlanSet()
 
     @property
     def k(self):
@@ -235,13 +235,15 @@ class PolarEncoder(nn.Module):
     def frozen_pos(self):
         return self._frozen_pos
 
-    def plan(self):
-        if self._plan is None:
-            self._plan = _lib.Plan(self._n, self._mask, 1, _lib.PL_F_MINSUM, flags=_lib.PL_PLAN_GENERIC)
-        return self._plan
+    def plan(self, device=None):
+        """The encoding plan on `device` (default: the current GPU); plans are device-bound."""
+        return self._plans.get(device, self._make_plan)
+
+    def _make_plan(self, dev):
+        return _lib.Plan(self._n, self._mask, 1, _lib.PL_F_MINSUM, flags=_lib.PL_PLAN_GENERIC, device=dev)
 
     def _encode_dev(self, u):
-        return ops.polar_encode(self.plan(), u)
+        return ops.polar_encode(self.plan(u.device), u)
 
     def forward(self, u):
         assert u.shape[-1] == self._k, "Last dim must be len k."

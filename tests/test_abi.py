@@ -133,3 +133,40 @@ def test_prebuilt_kernels_cover_the_reference_codes():
     have = set(os.listdir(build.KCACHE)) if os.path.isdir(build.KCACHE) else set()
     missing = [len(m) for m, fm in build.reference_codes() if _lib.sc_source(len(m), m, fm)[1] not in have]
     assert not missing, f"{len(missing)} specialised kernels not pre-built (run __graft_entry__.build())"
+
+
+def test_list_plan_limits_rejected_at_creation_without_gpu():
+    """SCL at n = 2048 needs list_size <= 16 (LDS-resident list state): L = 32 is refused by
+    pl_plan_create itself (PL_ENOTSUP, before any device call), and by the module constructors."""
+    import numpy as np
+    import torch
+    import polar_amd
+    from polar_amd import _lib, mysn
+    L = _lib.lib()
+    h = ctypes.c_void_p()
+    mask = np.zeros(2048, dtype=np.uint8)
+    mask[:1024] = 1
+    assert L.pl_plan_create(ctypes.byref(h), 2048, mask.ctypes.data_as(ctypes.c_void_p), 32, 0, 30.0, 0) == \
+        _lib.PL_ENOTSUP
+    assert b"list_size" in L.pl_last_error_string()
+    fp = torch.arange(1024)
+    for cls in (polar_amd.SCL_Dec, mysn.SCL_Dec):
+        with pytest.raises(ValueError):
+            cls(fp, 2048, list_size=32)
+    cls(fp, 2048, list_size=16)  # supported: no plan is built before the first forward
+    with pytest.raises(ValueError):
+        polar_amd.SC_Dec(torch.arange(2048), 4096)
+
+
+def test_generated_source_names_compiler_and_flags():
+    """The specialised kernel's source starts with the hipcc flags and the compiler the library
+    was built with (both part of the cache name); compile_code_object takes its flags from there."""
+    import numpy as np
+    from polar_amd import _lib
+    m = np.zeros(64, dtype=np.uint8)
+    m[:32] = 1
+    src, name = _lib.sc_source(64, m, 0)
+    flags, compiler = _lib._source_header(src)
+    assert "--genco" in flags and "--offload-arch=gfx950" in flags
+    assert compiler and compiler in _lib.hipcc_version(_lib.hipcc_path())
+    assert name.startswith("sc_") and name.endswith(".co")

@@ -145,3 +145,69 @@ def test_mysn_sc_module(pa):
     got = dec(torch.from_numpy(d["llr_awgn2"])).numpy().astype(np.uint8)
     assert got.shape == d["exact_awgn2"].shape
     assert (got != d["exact_awgn2"]).any(1).mean() <= 0.02
+
+
+@pytest.mark.parametrize("kernel", ["subtree", "generic"])
+@pytest.mark.parametrize("fast", [True, False])
+def test_mysn_scl_crc_llr_max_vs_oracle(pa, kernel, fast):
+    """llr_max != 30 (my_sn dec.py:213 self._llr_max): it clips f and the metric terms, sets the
+    dead-path metric (:420-422) and the CRC penalty llr_max*k (:517).  Min-sum f: bit-exact and
+    metrics to 1e-9 against the oracle run with the same llr_max, on both SCL kernels."""
+    from polar_amd import _lib, ops
+    from polar_amd.mysn import crc_params
+    k, n, L, lmax = 128, 256, 4, 7.5
+    fp = pa.reference_frozen_pos(k, n).numpy()
+    rng = np.random.default_rng(17)
+    u = oracle.crc_encode(rng.integers(0, 2, (160, k - 11)).astype(np.float32), "CRC11")
+    cw = oracle.polar_encode(u, fp, n)
+    llr = ((2 * cw - 1) * 2.5 + rng.standard_normal(cw.shape) * 3.0).astype(np.float32)
+    want, wpm = oracle.scl_decode_mysn(llr, fp, L, fast_scl=fast, exact_f=False, crc="CRC11", llr_max=lmax)
+    flags = (_lib.PL_PLAN_FAST_SCL if fast else 0) | (_lib.PL_PLAN_GENERIC if kernel == "generic" else 0)
+    plan = _lib.Plan(n, pa.frozen_mask(fp, n), L, _lib.PL_F_MINSUM, llr_max=lmax, flags=flags)
+    assert plan.kernel()[0] == ("scl_subtree" if kernel == "subtree" else "generic")
+    plan.set_crc(*crc_params("CRC11"))
+    got, pm = ops.scl_decode(plan, torch.from_numpy(llr).cuda(), return_pm=True)
+    assert np.array_equal(got.cpu().numpy(), want)
+    assert np.abs(pm.cpu().numpy() - wpm).max() < 1e-9
+    # the penalty really is llr_max*k: some row failed its CRC and carries it
+    assert (wpm.max(1) >= lmax * k).any()
+
+
+@pytest.mark.parametrize("L", [2, 8, 16])
+@pytest.mark.parametrize("fast", [False, True])
+def test_scl_n2048_vs_oracle(pa, L, fast):
+    """n = 2048 list decoding (generic kernel, list state in LDS up to L = 16): min-sum f,
+    bit-exact and metrics to 1e-9 against the oracle (x_run semantics without fast-SCL, my_sn
+    fast-SCL semantics with it)."""
+    from polar_amd import _lib, ops
+    n, k = 2048, 1024
+    fp = pa.reference_frozen_pos(k, n).numpy()
+    rng = np.random.default_rng(L + 3 * fast)
+    bs = 6 if L == 16 else 12
+    u = rng.integers(0, 2, (bs, k)).astype(np.float32)
+    cw = oracle.polar_encode(u, fp, n)
+    llr = ((2 * cw - 1) * 1.8 + rng.standard_normal(cw.shape) * 1.3).astype(np.float32)
+    llr[:, ::13] = np.round(llr[:, ::13])
+    if fast:
+        want, wpm = oracle.scl_decode_mysn(llr, fp, L, fast_scl=True, exact_f=False)
+    else:
+        want, wpm = oracle.scl_decode(llr, fp, L, lazy=True)
+    plan = _lib.Plan(n, pa.frozen_mask(fp, n), L, _lib.PL_F_MINSUM, flags=_lib.PL_PLAN_FAST_SCL if fast else 0)
+    assert plan.kernel()[0] == "generic"
+    got, pm = ops.scl_decode(plan, torch.from_numpy(llr).cuda(), return_pm=True)
+    assert np.array_equal(got.cpu().numpy(), want)
+    assert np.abs(pm.cpu().numpy() - wpm).max() < 1e-9
+
+
+def test_scl_n2048_module_and_limits(pa):
+    """The x_run SCL_Dec drop-in decodes n = 2048 (L <= 16) and rejects L = 32 at construction."""
+    n, k = 2048, 1024
+    fp = pa.reference_frozen_pos(k, n)
+    dec = pa.SCL_Dec(fp, n, list_size=4)
+    rng = np.random.default_rng(5)
+    x = torch.from_numpy((rng.standard_normal((3, n)) * 2).astype(np.float32))
+    want, wpm = oracle.scl_decode(x.numpy(), fp.numpy(), 4, lazy=True)
+    assert np.array_equal(dec(x).numpy(), want)
+    assert np.abs(dec.msg_pm - wpm).max() < 1e-9
+    with pytest.raises(ValueError, match="list_size"):
+        pa.SCL_Dec(fp, n, list_size=32)

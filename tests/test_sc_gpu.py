@@ -185,3 +185,29 @@ def test_sc_specialized_jit_for_an_arbitrary_code(pa, tmp_path, monkeypatch):
     assert _lib.Plan(n, pa.frozen_mask(fp, n), 1, 0, flags=_lib.PL_PLAN_CACHE_ONLY).kernel() == (kind, path)
     fp2 = np.sort(rng.permutation(n)[:401])
     assert _lib.Plan(n, pa.frozen_mask(fp2, n), 1, 0, flags=_lib.PL_PLAN_CACHE_ONLY).kernel()[0] == "generic"
+
+
+def test_plans_are_device_bound(pa):
+    """Plans record their device (pl_plan_device); modules keep one plan per device.  With two or
+    more GPUs: a plan refuses a stream of another device (PL_EINVAL -> ValueError), and a module
+    decodes on a non-current device with that device's own plan."""
+    import polar_amd
+    from polar_amd import _lib, ops
+    fp = polar_amd.reference_frozen_pos(128, 256)
+    p0 = _lib.Plan(256, pa.frozen_mask(fp.numpy(), 256), 1, 0, device=0)
+    assert p0.device == torch.device("cuda", 0)
+    dec = polar_amd.SC_Dec(fp, 256)
+    x = torch.randn((40, 256), generator=torch.Generator().manual_seed(3)) * 2
+    want = oracle.sc_decode(x.numpy(), fp.numpy())
+    assert np.array_equal(dec(x).numpy(), want)
+    assert np.array_equal(dec(x.cuda(0)).cpu().numpy(), want)
+    assert dec.plan(0).device == torch.device("cuda", 0)
+    if torch.cuda.device_count() < 2:
+        pytest.skip("one GPU: cross-device checks need two")
+    with torch.cuda.device(0):
+        got = dec(x.cuda(1))
+    assert got.device == torch.device("cuda", 1)
+    assert np.array_equal(got.cpu().numpy(), want)
+    assert dec.plan(1).device == torch.device("cuda", 1)
+    with pytest.raises(ValueError, match="device-bound"):
+        ops.sc_decode(p0, x.cuda(1))
