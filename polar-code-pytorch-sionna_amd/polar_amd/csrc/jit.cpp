@@ -186,7 +186,9 @@ std::string static_source(int n, const uint8_t* frozen, int f_mode) {
         std::vector<char> text;
         if (*alt && read_file(alt, text)) body.assign(text.begin(), text.end());
     }
-    o << body << "\nstruct PlCode {\n  static constexpr int N = " << n << ", LOG_N = " << log_n
+    int k = 0;
+    for (int i = 0; i < n; ++i) k += frozen[i] == 0;
+    o << body << "\nstruct PlCode {\n  static constexpr int N = " << n << ", K = " << k << ", LOG_N = " << log_n
       << ", LOG_G = " << lg << ", G = " << (1 << lg) << ", NS = " << (n >> lg) << ", FM = " << f_mode
       << ";\n  static constexpr unsigned char NT[" << nt.size() << "] = {";
     for (size_t i = 0; i < nt.size(); ++i) o << (i ? "," : "") << (int)nt[i];
@@ -275,10 +277,12 @@ int attach_static(pl_plan* p, const uint8_t* frozen, bool allow_compile) {
     hipFunction_t f32, u8;
     r = check_hip(hipModuleGetFunction(&f32, mod, "pl_sc_static_f32"), "hipModuleGetFunction");
     if (!r) r = check_hip(hipModuleGetFunction(&u8, mod, "pl_sc_static_u8"), "hipModuleGetFunction");
-    const int G = 1 << static_log_g(p->log_n, p->f_mode);
+    // info_loc[m]: where the u bit of information position m sits in a wave's LDS u words
+    // (sc_static.h emit): (byte offset of its word in codeword 0's area) << 5 | bit in the word
+    const int G = 1 << static_log_g(p->log_n, p->f_mode), WPL = (p->n / G + 31) / 32;
     std::vector<int32_t> loc;
     for (int i = 0; i < p->n; ++i)
-        if (!frozen[i]) loc.push_back((mirror_lane(G, i % G) << 8) | (i / G));
+        if (!frozen[i]) loc.push_back((((mirror_lane(G, i % G) * WPL + (i / G) / 32) * 4) << 5) | ((i / G) & 31));
     while (loc.size() % 4) loc.push_back(0);  // int4 reads of the table
     if (!r && !loc.empty()) {
         r = check_hip(hipMalloc(reinterpret_cast<void**>(&p->d_info_loc), loc.size() * sizeof(int32_t)),

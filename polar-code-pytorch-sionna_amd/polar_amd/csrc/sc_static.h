@@ -50,6 +50,12 @@ typedef unsigned long uintptr_t;
 #ifndef PL_SC_F_BITOP3
 #define PL_SC_F_BITOP3 0  // A/B on MI355X: 1 (explicit v_bitop3 sign merge) was slower
 #endif
+#ifndef PL_SC_F_BOUNDED
+#define PL_SC_F_BOUNDED 1  // min-sum f of a left child (inputs are f outputs, |x|, |y| <= llr_max) as one med3
+#endif
+#ifndef PL_SC_LANE31
+#define PL_SC_LANE31 1  // lane-level partial sums as bit-31-only flags (one-op hard decision, bitop3 combines)
+#endif
 #ifndef PL_SC_BIT31_ASM
 #define PL_SC_BIT31_ASM 0  // 1: opaque shift (no v_mul_lo fusion); measured slower overall
 #endif
@@ -74,6 +80,10 @@ typedef unsigned long uintptr_t;
 #ifndef PL_SC_PERSIST
 #define PL_SC_PERSIST 0  // 1: persistent software-pipelined waves (grid = resident waves)
 #endif
+// PL_SC_PERSIST 2: persistent waves whose next batch of channel rows is staged in LDS by an
+// asynchronous global->LDS copy (global_load_lds_dwordx4) while the current batch is decoded:
+// no channel-load latency on the critical path, 2 waves/SIMD (the staging takes 16 KiB of LDS
+// per wave at n = 1024).  Needs N >= 256 (whole 1-KiB copies per row).
 
 namespace pls {
 
@@ -95,6 +105,12 @@ using Beta = typename Cond<(E <= 32), uint32_t, uint64_t>::type;
 template <class C>
 constexpr int nt(int s, int p) {
     return C::NT[(C::N >> s) + (p >> s)];
+}
+// The stage-s node at position p is the left child of its parent: its input is the parent's f
+// output, bounded by llr_max in magnitude.
+template <class C>
+constexpr bool lchild(int s, int p) {
+    return s < C::LOG_N && ((p >> s) & 1) == 0;
 }
 
 template <int E>
@@ -118,10 +134,21 @@ __device__ __forceinline__ float mirf(float v) {
     return uf(mir<S>(fu(v)));
 }
 
+__device__ __forceinline__ float flip31(float x, uint32_t t);
+
 // f: polar_sc.py:46 (min-sum of clipped inputs) or my_sn dec.py:39-43 (exact boxplus).
-template <int FM>
+// BND: the inputs are known to satisfy |x|, |y| <= lmax -- they are the f outputs of the parent,
+// i.e. the node is a left child (lchild below) -- so the clip is the identity and
+//   sign(x) sign(y) min(|x|, |y|) = med3(-|x|, sign(x) y, |x|)
+// (y' = y with x's sign applied, clamped to [-|x|, |x|]): one bitop3 + one med3 instead of
+// min3 + xor + bitop3.  Exact: both pick an input magnitude; only the sign of a zero result can
+// differ, and no decision observes it (every test treats +0 and -0 alike).
+template <int FM, bool BND = false>
 __device__ __forceinline__ float fop(float x, float y, float lmax) {
     if constexpr (FM == 0) {
+#if PL_SC_F_BOUNDED
+        if constexpr (BND) return __builtin_amdgcn_fmed3f(-fabsf(x), flip31(y, fu(x)), fabsf(x));
+#endif
         const float m = fminf(fminf(fabsf(x), fabsf(y)), lmax);
 #if PL_SC_F_BITOP3
         // m | ((x ^ y) & sign): v_min3 + v_xor + v_bitop3 ((S0 & S1) | S2, table 0xEA)
@@ -152,8 +179,18 @@ __device__ __forceinline__ uint32_t bit31(W w, int j) {
 #endif
     return t;
 }
-// hard decision of a leaf, u = 1 iff !(llr > 0) (polar_sc.py:94-97), as a bit-31 flag
+// hard decision of a leaf, u = 1 iff !(llr > 0) (polar_sc.py:94-97), as a bit-31 flag.
+// PL_SC_LANE31: only bit 31 of a lane-level flag is meaningful (its consumers mask with the
+// lo31/hi31 lane masks or shift by 31), so the decision is one saturating subtract on the bit
+// pattern: bits(x) - 1 is negative iff bits(x) <= 0 as a signed integer, i.e. x <= +0 or x < 0
+// (no NaN), and the saturation keeps -0 (INT_MIN) negative.  No compare, no VCC.
+#if PL_SC_LANE31
+__device__ __forceinline__ uint32_t hd31(float x) {
+    return (uint32_t)__builtin_elementwise_sub_sat((int32_t)fu(x), (int32_t)1);
+}
+#else
 __device__ __forceinline__ uint32_t hd31(float x) { return (x > 0.0f) ? 0u : 0x80000000u; }
+#endif
 __device__ __forceinline__ uint32_t hd(float x) { return (x > 0.0f) ? 0u : 1u; }
 
 // wave-wide "any lane": the ballot builtin directly (hiprtc's __any materialises the predicate
@@ -162,7 +199,15 @@ __device__ __forceinline__ bool any_lane(bool p) { return __builtin_amdgcn_ballo
 __device__ __forceinline__ uint64_t ballot_lanes(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
 struct Lane {
-    uint32_t lom[5];  // lom[t]: all-ones if this lane holds the low element at level 2^t
+#if PL_SC_LANE31
+    // lo31[t] / hi31[t]: 0x80000000 if this lane holds the low / high element of its pair at
+    // level 2^t, else 0 (bitop3 operands; opaque to the compiler, see decode())
+    uint32_t lo31[5], hi31[5];
+    __device__ __forceinline__ uint32_t lom(int t) const { return (uint32_t)((int32_t)lo31[t] >> 31); }
+#else
+    uint32_t lom_[5];  // lom[t]: all-ones if this lane holds the low element at level 2^t
+    __device__ __forceinline__ uint32_t lom(int t) const { return lom_[t]; }
+#endif
     float lmax;
 };
 
@@ -207,15 +252,22 @@ template <class C, int s, int P>
 __device__ __forceinline__ uint32_t lsplit(float a, const Lane& ln) {
     constexpr int S = 1 << s;
     const float y = mirf<S>(a);
-    const uint32_t L = ln.lom[s];
     uint32_t bl = 0;
-    if constexpr (nt<C>(s - 1, P) != R0) bl = lnode<C, s - 1, P>(fop<C::FM>(a, y, ln.lmax), ln);
+    if constexpr (nt<C>(s - 1, P) != R0) bl = lnode<C, s - 1, P>(fop<C::FM, lchild<C>(s, P)>(a, y, ln.lmax), ln);
+#if PL_SC_LANE31
     // both lanes of the pair evaluate (1-2u) alpha_lo + alpha_hi: the low lane flips its own
-    // value, the high lane its partner's (bitop3 S1 ^ (S0 & S2) / S1 ^ (S0 & ~S2))
+    // value, the high lane its partner's (bitop3 S1 ^ (S0 & S2) with the lane's bit-31 mask)
+    const float x = uf(__builtin_amdgcn_bitop3_b32(bl, fu(a), ln.lo31[s], 0x6c)) +
+                    uf(__builtin_amdgcn_bitop3_b32(bl, fu(y), ln.hi31[s], 0x6c));
+    const uint32_t br = lnode<C, s - 1, P + S / 2>(x, ln);
+    return __builtin_amdgcn_bitop3_b32(bl, br, ln.lo31[s], 0x6c);  // br ^ (bl & lo31)
+#else
+    const uint32_t L = ln.lom(s);
     const float x = uf(__builtin_amdgcn_bitop3_b32(bl, fu(a), L, 0x6c)) +
                     uf(__builtin_amdgcn_bitop3_b32(bl, fu(y), L, 0x9c));
     const uint32_t br = lnode<C, s - 1, P + S / 2>(x, ln);
     return br ^ (bl & L);
+#endif
 }
 
 template <class C, int s, int P>
@@ -236,7 +288,11 @@ __device__ __forceinline__ uint32_t lnode(float a, const Lane& ln) {
         v = v + mirf<2>(v);
         return hd31(v);
     } else if constexpr (T == R1 && C::FM == 0) {
+#if PL_SC_LANE31
+        if (!any_lane(a == 0.0f)) return fu(a);  // bit 31 = the decision
+#else
         if (!any_lane(a == 0.0f)) return fu(a) & 0x80000000u;
+#endif
         return lsplit<C, s, P>(a, ln);
     } else if constexpr (T == SPC && C::FM == 0) {
         // magnitudes compared as integers (non-negative floats order like their bit patterns)
@@ -291,7 +347,7 @@ __device__ __forceinline__ Beta<(1 << s) / C::G> split(const float (&a)[(1 << s)
     BH bl = 0;
     if constexpr (nt<C>(s - 1, P) != R0) {
 #pragma unroll
-        for (int j = 0; j < H; ++j) x[j] = fop<C::FM>(a[j], a[j + H], ln.lmax);
+        for (int j = 0; j < H; ++j) x[j] = fop<C::FM, lchild<C>(s, P)>(a[j], a[j + H], ln.lmax);
         bl = child<C, s, P>(x, ln);
 #pragma unroll
         for (int j = 0; j < H; ++j) {
@@ -417,8 +473,8 @@ __device__ __forceinline__ Beta<C::NS / 2> half(float (&ch)[C::NS], uint64_t blr
         if constexpr (nt<C>(s - 1, P) != R0) {
 #pragma unroll
             for (int j = 0; j < H; ++j)
-                x[j] = fop<C::FM>(valpha<C>(ch, SIDE, blr, j, ln.lmax), valpha<C>(ch, SIDE, blr, j + H, ln.lmax),
-                                  ln.lmax);
+                x[j] = fop<C::FM, SIDE == 0>(valpha<C>(ch, SIDE, blr, j, ln.lmax),
+                                             valpha<C>(ch, SIDE, blr, j + H, ln.lmax), ln.lmax);
             bl = child<C, s, P>(x, ln);
         }
 #pragma unroll
@@ -471,65 +527,123 @@ __device__ __forceinline__ void to_u(uint64_t lo, uint64_t hi, const Lane& ln, u
     uint32_t w[4] = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
 #pragma unroll
     for (int i = 0; i < WPL; ++i) {
-        if constexpr (LG >= 4) w[i] ^= mir<16>(w[i]) & ln.lom[4];
-        if constexpr (LG >= 3) w[i] ^= mir<8>(w[i]) & ln.lom[3];
-        if constexpr (LG >= 2) w[i] ^= mir<4>(w[i]) & ln.lom[2];
-        if constexpr (LG >= 1) w[i] ^= mir<2>(w[i]) & ln.lom[1];
+        if constexpr (LG >= 4) w[i] ^= mir<16>(w[i]) & ln.lom(4);
+        if constexpr (LG >= 3) w[i] ^= mir<8>(w[i]) & ln.lom(3);
+        if constexpr (LG >= 2) w[i] ^= mir<4>(w[i]) & ln.lom(2);
+        if constexpr (LG >= 1) w[i] ^= mir<2>(w[i]) & ln.lom(1);
     }
 #pragma unroll
     for (int i = 0; i < WPL; ++i) mine[i] = w[i];
 }
 
 // Information bits of the wave's CW codewords (info_pos ascending, polar_sc.py:127) from its
-// LDS u words to coalesced output rows.  info_loc[m] = (lane-in-group << 8) | slot.
+// LDS u words to coalesced output rows.  info_loc[m] = (byte offset of the word holding info bit
+// m in codeword 0's u area) << 5 | bit (jit.cpp attach_static): one v_bfe_u32 extracts the bit
+// (its offset operand only reads bits 0-4), consecutive codewords are an immediate LDS offset
+// apart, and the K of the code is a compile-time constant (loops unrolled).  `il` holds this
+// lane's float4-path table entries when the caller preloaded them (PRE = true).
+template <class C>
+struct Emit {
+    static constexpr int CW = 64 / C::G, WPL = (C::NS + 31) / 32, CWB = C::G * WPL * 4;
+    static constexpr int KQ = C::K / 4, IT4 = (KQ + 63) / 64, IT1 = (C::K + 63) / 64;
+    static constexpr bool PRE = (C::K & 3) == 0 && IT4 <= 2;  // float4 table entries kept in VGPRs
+};
+
+// bit (e & 31) of the u word at byte address wa + row_off
+__device__ __forceinline__ float bitf(const unsigned char* wa, int e, int row_off) {
+    const uint32_t w = *reinterpret_cast<const uint32_t*>(wa + row_off);
+    return (float)__builtin_amdgcn_ubfe(w, (uint32_t)e, 1u);
+}
+
 template <class C, int OUT>
 __device__ __forceinline__ void emit(const uint32_t* __restrict__ ubase, int64_t cw0, int64_t bs, void* __restrict__ out,
-                                     const int32_t* __restrict__ info_loc, int k, int lane) {
-    constexpr int G = C::G, CW = 64 / G, WPL = (C::NS + 31) / 32;
-    if (OUT == OUT_F32 && (k & 3) == 0 && ((reinterpret_cast<uintptr_t>(out) & 15) == 0)) {
+                                     const int32_t* __restrict__ info_loc, const int4 (&il)[2], int lane) {
+    using E = Emit<C>;
+    constexpr int K = C::K, CW = E::CW, CWB = E::CWB;
+    const unsigned char* ub = reinterpret_cast<const unsigned char*>(ubase);
+    const bool full = cw0 + CW <= bs;  // wave-uniform
+    if (OUT == OUT_F32 && (K & 3) == 0 && ((reinterpret_cast<uintptr_t>(out) & 15) == 0)) {
         // 16-byte stores: lane writes info bits 4c..4c+3 of a row (1 KiB per wave-instruction)
-        const int kq = k >> 2;
-        for (int c = lane; c < kq; c += 64) {
-            const int4 l4 = reinterpret_cast<const int4*>(info_loc)[c];
-            const int lc[4] = {l4.x, l4.y, l4.z, l4.w};
-            int off[4], sh[4];
+        float* o = static_cast<float*>(out) + cw0 * K;
+        if constexpr (E::PRE) {
+            // every table entry is consumed before the first store: waiting for the preloaded
+            // entries then never waits for this wave's own output stores
+            const unsigned char* a[2][4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                off[i] = (lc[i] >> 8) * WPL + ((lc[i] & 255) >> 5);
-                sh[i] = lc[i] & 31;
+            for (int it = 0; it < E::IT4; ++it) {
+                int off[4] = {il[it].x >> 5, il[it].y >> 5, il[it].z >> 5, il[it].w >> 5};
+                // materialise now (the scheduler would sink the second iteration's offsets, and
+                // their wait, behind the first iteration's stores)
+                asm volatile("" : "+v"(off[0]), "+v"(off[1]), "+v"(off[2]), "+v"(off[3]));
+#pragma unroll
+                for (int i = 0; i < 4; ++i) a[it][i] = ub + off[i];
             }
 #pragma unroll
-            for (int g = 0; g < CW; ++g) {
-                const int64_t row = cw0 + g;
-                if (row < bs) {
-                    const uint32_t* src = ubase + g * G * WPL;
-                    float4 v;
-                    v.x = (float)((src[off[0]] >> sh[0]) & 1u);
-                    v.y = (float)((src[off[1]] >> sh[1]) & 1u);
-                    v.z = (float)((src[off[2]] >> sh[2]) & 1u);
-                    v.w = (float)((src[off[3]] >> sh[3]) & 1u);
-                    reinterpret_cast<float4*>(static_cast<float*>(out) + row * k)[c] = v;
+            for (int it = 0; it < E::IT4; ++it) {
+                const int c = lane + 64 * it;
+                if (E::KQ % 64 == 0 || c < E::KQ) {
+#pragma unroll
+                    for (int g = 0; g < CW; ++g) {
+                        if (full || cw0 + g < bs) {
+                            float4 v;
+                            v.x = bitf(a[it][0], il[it].x, g * CWB);
+                            v.y = bitf(a[it][1], il[it].y, g * CWB);
+                            v.z = bitf(a[it][2], il[it].z, g * CWB);
+                            v.w = bitf(a[it][3], il[it].w, g * CWB);
+                            reinterpret_cast<float4*>(o + g * K)[c] = v;
+                        }
+                    }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int it = 0; it < E::IT4; ++it) {
+                const int c = lane + 64 * it;
+                if (E::KQ % 64 == 0 || c < E::KQ) {
+                    const int4 l4 = reinterpret_cast<const int4*>(info_loc)[c];
+#pragma unroll
+                    for (int g = 0; g < CW; ++g) {
+                        if (full || cw0 + g < bs) {
+                            float4 v;
+                            v.x = bitf(ub + (l4.x >> 5), l4.x, g * CWB);
+                            v.y = bitf(ub + (l4.y >> 5), l4.y, g * CWB);
+                            v.z = bitf(ub + (l4.z >> 5), l4.z, g * CWB);
+                            v.w = bitf(ub + (l4.w >> 5), l4.w, g * CWB);
+                            reinterpret_cast<float4*>(o + g * K)[c] = v;
+                        }
+                    }
                 }
             }
         }
     } else {
-        for (int m = lane; m < k; m += 64) {
-            const int loc = info_loc[m];
-            const int l = loc >> 8, slot = loc & 255;
-            const uint32_t* src = ubase + l * WPL + (slot >> 5);
-            const int sh = slot & 31;
 #pragma unroll
-            for (int g = 0; g < CW; ++g) {
-                const int64_t row = cw0 + g;
-                if (row < bs) {
-                    const uint32_t bit = (src[g * G * WPL] >> sh) & 1u;
-                    if constexpr (OUT == OUT_F32) {
-                        static_cast<float*>(out)[row * k + m] = bit ? 1.0f : 0.0f;
-                    } else {
-                        static_cast<uint8_t*>(out)[row * k + m] = (uint8_t)bit;
+        for (int it = 0; it < E::IT1; ++it) {
+            const int m = lane + 64 * it;
+            if (K % 64 == 0 || m < K) {
+                const int e = info_loc[m];
+#pragma unroll
+                for (int g = 0; g < CW; ++g) {
+                    if (full || cw0 + g < bs) {
+                        const float b = bitf(ub + (e >> 5), e, g * CWB);
+                        if constexpr (OUT == OUT_F32) static_cast<float*>(out)[(cw0 + g) * K + m] = b;
+                        else static_cast<uint8_t*>(out)[(cw0 + g) * K + m] = (uint8_t)b;
                     }
                 }
             }
+        }
+    }
+}
+
+// this lane's float4-path table entries, loaded early (their latency hides behind the channel)
+template <class C>
+__device__ __forceinline__ void preload_info(const int32_t* __restrict__ info_loc, int4 (&il)[2], int lane) {
+    using E = Emit<C>;
+    il[0] = il[1] = int4{0, 0, 0, 0};
+    if constexpr (E::PRE) {
+#pragma unroll
+        for (int it = 0; it < E::IT4; ++it) {
+            const int c = lane + 64 * it;
+            if (E::KQ % 64 == 0 || c < E::KQ) il[it] = reinterpret_cast<const int4*>(info_loc)[c];
         }
     }
 }
@@ -589,12 +703,28 @@ __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs
                                        uint32_t* __restrict__ ulds) {
     constexpr int N = C::N, G = C::G, LG = C::LOG_G, NS = C::NS, CW = 64 / G;
     constexpr int WPL = (NS + 31) / 32;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // the wave index is wave-uniform: as an SGPR value all batch/row address math is scalar
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int q = lane & (G - 1);
     Lane ln;
     int res;
-    lane_layout<LG>(q, res, ln.lom);
-    ln.lom[0] = 0u;
+#if PL_SC_LANE31
+    {
+        uint32_t lom[5];
+        lane_layout<LG>(q, res, lom);
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+            ln.lo31[t] = t ? lom[t] & 0x80000000u : 0u;
+            ln.hi31[t] = t ? ~lom[t] & 0x80000000u : 0u;
+            // keep them VGPR values: a mask the compiler knows to be 0/~0 per lane becomes an
+            // SGPR lane mask and each combine a v_cndmask + v_xor instead of one v_bitop3
+            asm volatile("" : "+v"(ln.lo31[t]), "+v"(ln.hi31[t]));
+        }
+    }
+#else
+    lane_layout<LG>(q, res, ln.lom_);
+    ln.lom_[0] = 0u;
+#endif
     ln.lmax = lmax;
     uint32_t* ubase = ulds + wave * 64 * WPL;
     uint32_t* mine = ulds + (wave * 64 + lane) * WPL;
@@ -606,6 +736,8 @@ __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs
     // the tree and the output of this batch instead of stalling every wave at the same instant.
     const int64_t stride = (int64_t)gridDim.x * kWaves * CW;
     int64_t cw0 = ((int64_t)blockIdx.x * kWaves + wave) * CW;
+    int4 il[2];
+    preload_info<C>(info_loc, il, lane);
     float chv[NS];
     load_channel<C>(chv, llr, cw0, bs, lane, res);
     for (; cw0 < bs; cw0 += stride) {
@@ -614,7 +746,7 @@ __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs
         root_virtual<C>(chv, ln, lo, hi, Refill<C>{chv, llr, ncw0, bs, lane, res});
         to_u<C>(lo, hi, ln, mine);
         wave_lds_fence();
-        emit<C, OUT>(ubase, cw0, bs, out, info_loc, k, lane);
+        emit<C, OUT>(ubase, cw0, bs, out, info_loc, il, lane);
         wave_lds_fence();
     }
 #else
@@ -625,6 +757,8 @@ __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs
     uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
 #endif
     uint64_t lo = 0, hi = 0;
+    int4 il[2];
+    preload_info<C>(info_loc, il, lane);
 #if PL_SC_ROOT_MODE == 0
     float chv[NS];
     load_channel<C>(chv, llr, cw0, bs, lane, res);
@@ -679,7 +813,7 @@ __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs
 #if PL_SC_STAMPS
     uint64_t st3 = __builtin_amdgcn_s_memtime();
 #endif
-    emit<C, OUT>(ubase, cw0, bs, out, info_loc, k, lane);
+    emit<C, OUT>(ubase, cw0, bs, out, info_loc, il, lane);
 #if PL_SC_STAMPS
     __builtin_amdgcn_s_waitcnt(0);
     uint64_t st4 = __builtin_amdgcn_s_memtime();
@@ -695,22 +829,138 @@ __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs
 #endif
 }
 
+
+#if PL_SC_PERSIST == 2
+// LDS layout of the staged kernel (one __shared__ array: a second LDS object can make the
+// compiler drain the copies early): [kWaves][64 lanes][WPL] u words, then per wave CW channel
+// rows of N floats + a 16-float pad (rows r and r + 1 start in opposite halves of the 32 banks,
+// so the ds_read_b32 of the residue layout is conflict-free).
+template <class C>
+struct Staged {
+    static constexpr int CW = 64 / C::G, WPL = (C::NS + 31) / 32, ROW = C::N + 16;
+    static constexpr int U_WORDS = kWaves * 64 * WPL;
+    static constexpr int WORDS = U_WORDS + kWaves * CW * ROW;
+    static constexpr int COPIES = CW * (C::N / 256);  // 1-KiB copies per batch
+    static constexpr int KQ = C::K / 4;               // float4 output chunks per row
+    static constexpr int IT4 = (KQ + 63) / 64, IT1 = (C::K + 63) / 64;
+    // store instructions one batch's emit issues after the next batch's copies (full batches):
+    // the counted wait before reading the staging buffer leaves exactly these outstanding
+    static constexpr int ST_VEC = IT4 * CW, ST_SCALAR = IT1 * CW;
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+    static_assert(N >= 0, "");
+    if constexpr (N >= 63) asm volatile("s_waitcnt vmcnt(63)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Rows cw0 .. cw0+CW-1 (clamped to bs-1) into the wave's staging rows, 1 KiB per instruction.
+template <class C>
+__device__ __forceinline__ void stage_copy(const float* __restrict__ llr, int64_t cw0, int64_t bs, float* rows,
+                                           int lane) {
+    using S = Staged<C>;
+#pragma unroll
+    for (int r = 0; r < S::CW; ++r) {
+        const int64_t cw = cw0 + r < bs ? cw0 + r : bs - 1;
+        const float* src = llr + (size_t)cw * C::N + lane * 4;
+#pragma unroll
+        for (int i = 0; i < C::N / 256; ++i)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + i * 256),
+                                             (__attribute__((address_space(3))) void*)(rows + r * S::ROW + i * 256),
+                                             16, 0, 0);
+    }
+}
+
+template <class C, int OUT>
+__device__ __forceinline__ void decode_staged(const float* __restrict__ llr, int64_t bs, void* __restrict__ out,
+                                              const int32_t* __restrict__ info_loc, int k, float lmax,
+                                              uint32_t* __restrict__ lds) {
+    using S = Staged<C>;
+    constexpr int G = C::G, LG = C::LOG_G, NS = C::NS, CW = S::CW, WPL = S::WPL;
+    static_assert(C::N >= 256 && C::N % 256 == 0, "staged channel rows are whole 1-KiB copies");
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int q = lane & (G - 1);
+    Lane ln;
+    int res;
+#if PL_SC_LANE31
+    {
+        uint32_t lom[5];
+        lane_layout<LG>(q, res, lom);
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+            ln.lo31[t] = t ? lom[t] & 0x80000000u : 0u;
+            ln.hi31[t] = t ? ~lom[t] & 0x80000000u : 0u;
+            asm volatile("" : "+v"(ln.lo31[t]), "+v"(ln.hi31[t]));
+        }
+    }
+#else
+    lane_layout<LG>(q, res, ln.lom_);
+    ln.lom_[0] = 0u;
+#endif
+    ln.lmax = lmax;
+    uint32_t* ubase = lds + wave * 64 * WPL;
+    uint32_t* mine = lds + (wave * 64 + lane) * WPL;
+    float* rows = reinterpret_cast<float*>(lds + S::U_WORDS) + wave * CW * S::ROW;
+    const float* myrow = rows + (lane >> LG) * S::ROW + res;
+    const bool vec = OUT == OUT_F32 && (C::K & 3) == 0 && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
+
+    const int64_t stride = (int64_t)gridDim.x * kWaves * CW;
+    int64_t cw0 = ((int64_t)blockIdx.x * kWaves + wave) * CW;
+    if (cw0 >= bs) return;  // wave-uniform; no block-wide barrier below
+    int4 il[2];
+    preload_info<C>(info_loc, il, lane);
+    stage_copy<C>(llr, cw0, bs, rows, lane);
+    wait_vm<0>();
+    for (;;) {
+        float chv[NS];
+#pragma unroll
+        for (int j = 0; j < NS; ++j) chv[j] = myrow[j * G];
+        // the reads must have returned before the next copy overwrites the rows
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const int64_t ncw0 = cw0 + stride;
+        const bool more = ncw0 < bs;
+        if (more) stage_copy<C>(llr, ncw0, bs, rows, lane);
+        uint64_t lo = 0, hi = 0;
+        root_virtual<C>(chv, ln, lo, hi, NoHook());
+        to_u<C>(lo, hi, ln, mine);
+        wave_lds_fence();
+        emit<C, OUT>(ubase, cw0, bs, out, info_loc, il, lane);
+        wave_lds_fence();
+        if (!more) break;
+        // this batch was full (a partial batch is the last one): its emit issued exactly
+        // ST_VEC / ST_SCALAR stores after the copies
+        if (vec) wait_vm<S::ST_VEC>();
+        else wait_vm<S::ST_SCALAR>();
+        cw0 = ncw0;
+    }
+    (void)k;
+}
+#endif
+
 }  // namespace pls
 
 // Entry points instantiated per code: the including translation unit defines PlCode first.
+#if PL_SC_PERSIST == 2
+#define PL_SC_ENTRY(CODE, NAME, OUTK)                                                                        \
+    extern "C" __global__ __launch_bounds__(64 * pls::kWaves, 2) void NAME(                                  \
+        const float* __restrict__ llr, int64_t bs, void* __restrict__ out, const int32_t* __restrict__ info_loc, \
+        int k, float lmax) {                                                                                  \
+        __shared__ uint32_t lds[pls::Staged<CODE>::WORDS];                                                   \
+        pls::decode_staged<CODE, OUTK>(llr, bs, out, info_loc, k, lmax, lds);                                \
+    }
+#else
+#define PL_SC_ENTRY(CODE, NAME, OUTK)                                                                        \
+    extern "C" __global__ __launch_bounds__(64 * pls::kWaves, PL_SC_MINW) void NAME(                         \
+        const float* __restrict__ llr, int64_t bs, void* __restrict__ out, const int32_t* __restrict__ info_loc, \
+        int k, float lmax) {                                                                                  \
+        __shared__ uint32_t ulds[pls::kWaves * 64 * ((CODE::NS + 31) / 32)];                                 \
+        pls::decode<CODE, OUTK>(llr, bs, out, info_loc, k, lmax, ulds);                                      \
+    }
+#endif
 #define PL_SC_STATIC_KERNELS(CODE)                                                                           \
     extern "C" __device__ const int pl_sc_persistent = PL_SC_PERSIST;                                       \
-    extern "C" __global__ __launch_bounds__(64 * pls::kWaves, PL_SC_MINW) void pl_sc_static_f32(                      \
-        const float* __restrict__ llr, int64_t bs, void* __restrict__ out, const int32_t* __restrict__ info_loc, \
-        int k, float lmax) {                                                                                  \
-        __shared__ uint32_t ulds[pls::kWaves * 64 * ((CODE::NS + 31) / 32)];                                 \
-        pls::decode<CODE, pls::OUT_F32>(llr, bs, out, info_loc, k, lmax, ulds);               \
-    }                                                                                                        \
-    extern "C" __global__ __launch_bounds__(64 * pls::kWaves, PL_SC_MINW) void pl_sc_static_u8(                       \
-        const float* __restrict__ llr, int64_t bs, void* __restrict__ out, const int32_t* __restrict__ info_loc, \
-        int k, float lmax) {                                                                                  \
-        __shared__ uint32_t ulds[pls::kWaves * 64 * ((CODE::NS + 31) / 32)];                                 \
-        pls::decode<CODE, pls::OUT_U8>(llr, bs, out, info_loc, k, lmax, ulds);                \
-    }
+    PL_SC_ENTRY(CODE, pl_sc_static_f32, pls::OUT_F32)                                                        \
+    PL_SC_ENTRY(CODE, pl_sc_static_u8, pls::OUT_U8)
 
 #endif  // PL_SC_STATIC_H

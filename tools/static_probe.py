@@ -57,7 +57,8 @@ def lam(G):
 def info_loc(mask, name=None):
     n = len(mask); G = 1 << lg_of(n, name); L = lam(G)
     pos = np.nonzero(mask == 0)[0]
-    return np.array([(L[p % G] << 8) | (p // G) for p in pos], dtype=np.int32)
+    WPL = (n // G + 31) // 32  # sc_static.h emit encoding (jit.cpp attach_static)
+    return np.array([(((L[p % G] * WPL + (p // G) // 32) * 4) << 5) | ((p // G) & 31) for p in pos], dtype=np.int32)
 
 def code_src(mask, fm=0, name=None):
     n = len(mask); logn = n.bit_length() - 1; lg = lg_of(n, name)
