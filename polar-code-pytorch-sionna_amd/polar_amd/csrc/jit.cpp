@@ -143,8 +143,12 @@ std::vector<uint8_t> node_types(int n, const uint8_t* frozen) {
 // n = 2048 already uses the widest group (16 lanes).
 bool tuned_wide(int log_n, int f_mode) { return f_mode == PL_F_MINSUM && log_n >= 8 && log_n <= 10; }
 
-// log2(lanes per codeword)
+// log2(lanes per codeword); PL_SC_LOG_G overrides it (development A/B: part of the source)
 int static_log_g(int log_n, int f_mode) {
+    if (const char* e = getenv("PL_SC_LOG_G")) {
+        const int v = atoi(e);
+        if (v >= 0 && v <= 4 && v <= log_n) return v;
+    }
     if (tuned_wide(log_n, f_mode)) return log_n - 6;
     return log_n > 7 ? log_n - 7 : 0;
 }
@@ -279,7 +283,8 @@ int attach_static(pl_plan* p, const uint8_t* frozen, bool allow_compile) {
     if (!r) r = check_hip(hipModuleGetFunction(&u8, mod, "pl_sc_static_u8"), "hipModuleGetFunction");
     // info_loc[m]: where the u bit of information position m sits in a wave's LDS u words
     // (sc_static.h emit): (byte offset of its word in codeword 0's area) << 5 | bit in the word
-    const int G = 1 << static_log_g(p->log_n, p->f_mode), WPL = (p->n / G + 31) / 32;
+    const int lg = static_log_g(p->log_n, p->f_mode);
+    const int G = 1 << lg, WPL = (p->n / G + 31) / 32;
     std::vector<int32_t> loc;
     for (int i = 0; i < p->n; ++i)
         if (!frozen[i]) loc.push_back((((mirror_lane(G, i % G) * WPL + (i / G) / 32) * 4) << 5) | ((i / G) & 31));
@@ -305,6 +310,7 @@ int attach_static(pl_plan* p, const uint8_t* frozen, bool allow_compile) {
     int dev = 0, cus = 0;
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+    p->sc_log_g = lg;
     p->sc_persistent = persistent;
     p->resident_blocks = 2 * cus;
     p->sc_module = mod;
@@ -322,7 +328,7 @@ void detach_static(pl_plan* p) {
 
 int launch_sc_static(const pl_plan* p, const float* llr, int64_t bs, void* out, int out_kind, hipStream_t st) {
     if (bs == 0 || p->k == 0) return PL_OK;
-    const int G = 1 << static_log_g(p->log_n, p->f_mode);
+    const int G = 1 << p->sc_log_g;           // the layout the plan's kernel was built for
     const int64_t per_block = 4 * (64 / G);  // pls::kWaves codeword groups of 64/G
     int64_t blocks = (bs + per_block - 1) / per_block;
     if (p->sc_persistent && p->resident_blocks > 0 && blocks > p->resident_blocks) blocks = p->resident_blocks;

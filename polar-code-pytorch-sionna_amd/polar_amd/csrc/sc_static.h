@@ -56,6 +56,9 @@ typedef unsigned long uintptr_t;
 #ifndef PL_SC_LANE31
 #define PL_SC_LANE31 1  // lane-level partial sums as bit-31-only flags (one-op hard decision, bitop3 combines)
 #endif
+#ifndef PL_SC_EMIT_PRE
+#define PL_SC_EMIT_PRE 1  // preload the output table entries at kernel start (8 VGPRs)
+#endif
 #ifndef PL_SC_BIT31_ASM
 #define PL_SC_BIT31_ASM 0  // 1: opaque shift (no v_mul_lo fusion); measured slower overall
 #endif
@@ -73,6 +76,12 @@ typedef unsigned long uintptr_t;
 #endif
 #ifndef PL_SC_DIAG_SKIP_LANE
 #define PL_SC_DIAG_SKIP_LANE 0
+#endif
+#ifndef PL_SC_DIAG_NO_LOAD
+#define PL_SC_DIAG_NO_LOAD 0
+#endif
+#ifndef PL_SC_DIAG_NO_TREE
+#define PL_SC_DIAG_NO_TREE 0
 #endif
 #ifndef PL_SC_DIAG_SKIP_SPECIAL
 #define PL_SC_DIAG_SKIP_SPECIAL 0
@@ -546,7 +555,7 @@ template <class C>
 struct Emit {
     static constexpr int CW = 64 / C::G, WPL = (C::NS + 31) / 32, CWB = C::G * WPL * 4;
     static constexpr int KQ = C::K / 4, IT4 = (KQ + 63) / 64, IT1 = (C::K + 63) / 64;
-    static constexpr bool PRE = (C::K & 3) == 0 && IT4 <= 2;  // float4 table entries kept in VGPRs
+    static constexpr bool PRE = PL_SC_EMIT_PRE && (C::K & 3) == 0 && IT4 <= 2;  // table entries kept in VGPRs
 };
 
 // bit (e & 31) of the u word at byte address wa + row_off
@@ -761,13 +770,29 @@ __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs
     preload_info<C>(info_loc, il, lane);
 #if PL_SC_ROOT_MODE == 0
     float chv[NS];
+#if PL_SC_DIAG_NO_LOAD  // diagnostic only (wrong results): the tree without the channel loads
+#pragma unroll
+    for (int j = 0; j < NS; ++j) chv[j] = (float)((lane * 7 + j * 13) % 61) - 30.5f;
+    asm volatile("" ::"v"(llr));
+#else
     load_channel<C>(chv, llr, cw0, bs, lane, res);
+#endif
 #if PL_SC_STAMPS
     __builtin_amdgcn_s_waitcnt(0);
     for (int j = 0; j < NS; ++j) asm volatile("" : "+v"(chv[j]));
     uint64_t st1 = __builtin_amdgcn_s_memtime();
 #endif
+#if PL_SC_DIAG_NO_TREE  // diagnostic only (wrong results): loads and output without the tree
+    {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) acc ^= fu(chv[j]) << (j & 31);
+        lo = acc;
+        hi = acc >> 1;
+    }
+#else
     root_virtual<C>(chv, ln, lo, hi, NoHook());
+#endif
 #else
     // Stage LOG_N-1 held in VGPRs; the channel is read once per half (the second read is
     // served by the caches) and is never live across a half's subtree.

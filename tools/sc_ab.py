@@ -27,6 +27,14 @@ def _env(spec):
     src = ""
     if spec.startswith("@"):
         src, _, spec = spec[1:].partition(" ")
+    # "LOG_G=k" in a spec selects the lanes per codeword (jit.cpp PL_SC_LOG_G), not a macro
+    toks = spec.split()
+    lg = [t for t in toks if t.startswith("LOG_G=")]
+    spec = " ".join(t for t in toks if not t.startswith("LOG_G="))
+    if lg:
+        os.environ["PL_SC_LOG_G"] = lg[0].split("=")[1]
+    else:
+        os.environ.pop("PL_SC_LOG_G", None)
     if spec:
         os.environ["PL_SC_DEFINES"] = spec
     else:
@@ -75,7 +83,7 @@ def build(names, k, n, fm):
             print(*r, flush=True)
 
 
-def run(names, k, n, fm, rounds, bs):
+def run(names, k, n, fm, rounds, bs, only=False):
     import torch
 
     import polar_amd
@@ -93,7 +101,7 @@ def run(names, k, n, fm, rounds, bs):
     x3 = torch.round(x2 * 2) / 2
     x4 = (x2 * 40).contiguous()
     plans = {}
-    for name in ["base"] + [v for v in names if v != "base"]:
+    for name in (names if only else ["base"] + [v for v in names if v != "base"]):
         _env(specs[name])
         p = _lib.Plan(n, m, 1, fm, flags=_lib.PL_PLAN_CACHE_ONLY)
         kind, path = p.kernel()
@@ -104,7 +112,7 @@ def run(names, k, n, fm, rounds, bs):
     _env("")
     out = torch.empty((bs, k), device=dev)
     gplan = _lib.Plan(n, m, 1, fm, flags=_lib.PL_PLAN_GENERIC)  # independent kernel as the reference
-    for name, p in plans.items():
+    for name, p in ({} if only else plans).items():
         bad = 0
         for x in (llr, x2, x3, x4):
             want = ops.sc_decode(gplan, x)
@@ -112,7 +120,7 @@ def run(names, k, n, fm, rounds, bs):
             bad += int((got != want).any(dim=1).sum())
         print(f"{name}: {'exact' if bad == 0 else f'{bad} MISMATCHING ROWS'} vs the generic kernel", flush=True)
 
-    def tm(p, reps=200):
+    def tm(p, reps=20 if only else 200):
         for _ in range(20):
             ops.sc_decode(p, llr, out=out)
         torch.cuda.synchronize()
@@ -124,8 +132,9 @@ def run(names, k, n, fm, rounds, bs):
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / reps
     # settle the clock
-    for _ in range(2000):
-        ops.sc_decode(plans["base"], llr, out=out)
+    first = next(iter(plans.values()))
+    for _ in range(20 if only else 2000):
+        ops.sc_decode(first, llr, out=out)
     res = {nm: [] for nm in plans}
     for r in range(rounds):
         for nm, p in plans.items():
@@ -133,8 +142,8 @@ def run(names, k, n, fm, rounds, bs):
     for nm, ts in res.items():
         ts = sorted(ts)
         med = ts[len(ts) // 2]
-        print(f"{nm:24s} median {med:.4f} ms  min {ts[0]:.4f}  {bs / med / 1e3:.1f} Mcw/s  "
-              f"({med / sorted(res['base'])[len(ts) // 2]:.3f}x base)", flush=True)
+        rel = f"({med / sorted(res['base'])[len(ts) // 2]:.3f}x base)" if "base" in res else ""
+        print(f"{nm:24s} median {med:.4f} ms  min {ts[0]:.4f}  {bs / med / 1e3:.1f} Mcw/s  {rel}", flush=True)
 
 
 if __name__ == "__main__":
@@ -146,8 +155,9 @@ if __name__ == "__main__":
     ap.add_argument("--fm", type=int, default=0)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--bs", type=int, default=65536)
+    ap.add_argument("--only", action="store_true", help="run: time the named variants only (no base, no check)")
     a = ap.parse_args()
     if a.cmd == "build":
         build(a.names, a.k, a.n, a.fm)
     else:
-        run(a.names, a.k, a.n, a.fm, a.rounds, a.bs)
+        run(a.names, a.k, a.n, a.fm, a.rounds, a.bs, a.only)
