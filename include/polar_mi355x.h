@@ -144,6 +144,21 @@ int pl_gather_rows(const float* in, int64_t bs, int32_t n_in, const int32_t* idx
 int pl_rate_recover(const float* llr, int64_t bs, int32_t e, const int32_t* src_a, const int32_t* src_b,
                     const float* fill, int32_t n, float* out, void* hip_stream);
 
+/* Monte-Carlo caller side, fused (polar_amd.channel.FusedAWGN, polar_amd.sim):
+ * pl_awgn_qpsk_llr: System_AWGN_model.forward up to the decoder call (x_run_sn_polar/z_sys_model/
+ *                  awgn_model.py:33-41) for rows row0 .. row0+bs-1 of a random stream: information bits
+ *                  (BinarySource, my_sn/trans/binary_source.py:18-19; Philox4x32-10 keyed by seed,
+ *                  counter (row, iteration)), codeword x = u G_n with the plan's frozen set
+ *                  (x_run enc.py:30-43), Gray QPSK (mapping.py:136-149), AWGN of variance no
+ *                  (awgn.py:19-29), logits log P(b=1)/P(b=0) (mapping.py:225-241).
+ *                  u_out (nullable): [bs, k] fp32 0/1; llr_out: [bs, n] fp32.  no > 0.
+ * pl_count_errors: count_errors + count_block_errors (my_sn/sim.py:7-18) of two [rows, k] fp32 0/1
+ *                  tensors: counts[0] += differing elements, counts[1] += rows with a difference
+ *                  (int64 device counters, accumulated). */
+int pl_awgn_qpsk_llr(const pl_plan* plan, uint64_t seed, uint64_t iteration, int64_t row0, int64_t bs, float no,
+                     float* u_out, float* llr_out, void* hip_stream);
+int pl_count_errors(const float* a, const float* b, int64_t rows, int32_t k, int64_t* counts, void* hip_stream);
+
 const char* pl_last_error_string(void);
 const char* pl_version(void);
 

@@ -17,7 +17,8 @@ CSRC = os.path.join(HERE, "csrc")
 OBJ = os.path.join(HERE, "_obj")
 LIB = os.path.join(HERE, "libpolar_mi355x.so")
 KCACHE = os.path.join(HERE, "kcache")
-SOURCES = ["sc_kernel.hip", "scl_kernel.hip", "encode_kernel.hip", "ratematch_kernel.hip", "capi.cpp", "jit.cpp"]
+SOURCES = ["sc_kernel.hip", "scl_kernel.hip", "encode_kernel.hip", "ratematch_kernel.hip", "channel_kernel.hip",
+           "capi.cpp", "jit.cpp"]
 # scl_tree_kernel.hip is compiled once per list size (its instantiations, in parallel) and once
 # for the launcher: (object name, source, defines)
 UNITS = [(s + ".o", s, []) for s in SOURCES] + \
@@ -79,7 +80,7 @@ def build(force=False, verbose=False):
     with ThreadPoolExecutor(max_workers=min(8, len(jobs) or 1)) as ex:
         list(ex.map(run, jobs))
     objs = [os.path.join(OBJ, u[0]) for u in UNITS]
-    if force or jobs or not os.path.exists(LIB):
+    if force or jobs or not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs):
         cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, f"-L{ROCM}/lib",
                f"-Wl,-rpath,{ROCM}/lib", "-lhiprtc", "-o", LIB]
         r = subprocess.run(cmd, capture_output=True, text=True)

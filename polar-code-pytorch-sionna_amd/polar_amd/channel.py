@@ -11,6 +11,11 @@ the CPU device it reproduces the reference's LLRs bit for bit (pinned by tests/g
   System_AWGN_model  x_run_sn_polar/z_sys_model/awgn_model.py:17-44
 On a GPU the same ops run on device (different RNG stream, same distribution) and the encoder is
 the HIP XOR-butterfly kernel (bit-identical to the reference's dense c@G % 2, enc.py:42).
+
+FusedAWGN is the same system model as ONE HIP kernel (pl_awgn_qpsk_llr, csrc/channel_kernel.hip):
+Philox4x32-10 bits and noise, encoder, mapper, channel and demapper fused -- the production
+producer on a GPU (statistical parity with the reference; System_AWGN_model keeps the op-by-op
+numerics and RNG order for the CPU-device reproduction of the reference).
 """
 import numpy as np
 import torch as tc
@@ -191,3 +196,88 @@ class System_AWGN_model(nn.Module):
         if self.cw_estimates:
             return codewords, bits_hat
         return bits, bits_hat
+
+
+class FusedAWGN(nn.Module):
+    """System_AWGN_model (awgn_model.py:17-44) with the whole producer -- bits, polar encoder, QPSK
+    mapper, AWGN, demapper -- as one HIP kernel per call (pl_awgn_qpsk_llr).
+
+    Same interface: forward(batch_size, ebno_db) -> (bits, bits_hat) (or (codewords=None, bits_hat)
+    with cw_estimates), llrs(batch_size, ebno_db) -> (bits, None, logits).  Randomness is Philox
+    keyed by `seed`; every call draws a fresh iteration of the stream (`iteration` counts calls),
+    and `row0` offsets the rows (a rank's shard of a multi-GPU batch)."""
+
+    def __init__(self, n, k, frozen_pos, decoder, device=None, seed=42, row0=0, cw_estimates=False):
+        super().__init__()
+        from . import _lib
+        from .frozen import frozen_mask
+        self.n, self.k = int(n), int(k)
+        self.n_bits_per_sym = 2
+        self.coderate = self.k / self.n
+        self.decoder = decoder
+        self.cw_estimates = cw_estimates
+        self.seed, self.row0, self.iteration = int(seed), int(row0), 0
+        self._mask = frozen_mask(frozen_pos, self.n)
+        assert self.n - int(self._mask.sum()) == self.k, "k must equal n - len(frozen_pos)"
+        self.device = tc.device(device) if device is not None else tc.device("cuda", tc.cuda.current_device())
+        self._plans = _lib.PlanSet()
+
+    def _make_plan(self, dev):
+        from . import _lib
+        return _lib.Plan(self.n, self._mask, 1, flags=_lib.PL_PLAN_GENERIC, device=dev)
+
+    def llrs(self, batch_size, ebno_db):
+        from . import ops
+        no = float(ebnodb2no(float(ebno_db), self.n_bits_per_sym, self.coderate))
+        it = self.iteration
+        self.iteration += 1
+        bits, llr = ops.awgn_qpsk_llr(self._plans.get(self.device, self._make_plan), int(batch_size), no,
+                                      self.seed, it, self.row0)
+        return bits, None, llr
+
+    def forward(self, batch_size, ebno_db):
+        bits, _, llr = self.llrs(batch_size, ebno_db)
+        bits_hat = self.decoder(llr)
+        if self.cw_estimates:
+            return None, bits_hat
+        return bits, bits_hat
+
+
+def philox4x32_10(ctr, key):
+    """Random123 Philox4x32-10 on numpy uint32 arrays: ctr [..., 4], key [..., 2] -> [..., 4].
+    The host restatement of csrc/channel_kernel.hip's generator (tests pin the kernel's bit
+    placement against it; the Random123 known-answer vectors pin this function)."""
+    c = np.array(ctr, dtype=np.uint64)
+    k0 = np.array(key[..., 0], dtype=np.uint64)
+    k1 = np.array(key[..., 1], dtype=np.uint64)
+    m32 = np.uint64(0xFFFFFFFF)
+    for _ in range(10):
+        p0 = np.uint64(0xD2511F53) * c[..., 0]
+        p1 = np.uint64(0xCD9E8D57) * c[..., 2]
+        hi0, lo0 = p0 >> np.uint64(32), p0 & m32
+        hi1, lo1 = p1 >> np.uint64(32), p1 & m32
+        c = np.stack([hi1 ^ c[..., 1] ^ k0, lo1, hi0 ^ c[..., 3] ^ k1, lo0], axis=-1)
+        k0 = (k0 + np.uint64(0x9E3779B9)) & m32
+        k1 = (k1 + np.uint64(0xBB67AE85)) & m32
+    return c.astype(np.uint32)
+
+
+def fused_info_bits(seed, iteration, rows, k):
+    """The information bits pl_awgn_qpsk_llr draws for stream rows `rows` (1-D int64): bit r of a
+    row is bit r % 32 of Philox word r // 32, word q = component q % 4 of the block with counter
+    (row, iteration, q // 4) -- returned as float32 [len(rows), k]."""
+    rows = np.asarray(rows, dtype=np.int64).reshape(-1)
+    nq = (k + 31) // 32
+    q = np.arange(nq)
+    ctr = np.zeros((len(rows), nq, 4), dtype=np.uint64)
+    ctr[..., 0] = (rows & 0xFFFFFFFF)[:, None]
+    ctr[..., 1] = (rows >> 32)[:, None]
+    ctr[..., 2] = np.uint64(iteration & 0xFFFFFFFF)
+    ctr[..., 3] = (q >> 2)[None, :]
+    key = np.zeros((len(rows), nq, 2), dtype=np.uint64)
+    key[..., 0] = seed & 0xFFFFFFFF
+    key[..., 1] = (seed >> 32) & 0xFFFFFFFF
+    words = philox4x32_10(ctr, key)               # [rows, nq, 4]
+    w = words[:, q, q & 3]                        # [rows, nq]
+    bits = (w[..., None] >> np.arange(32, dtype=np.uint32)) & 1
+    return bits.reshape(len(rows), nq * 32)[:, :k].astype(np.float32)

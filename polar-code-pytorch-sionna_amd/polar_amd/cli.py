@@ -41,6 +41,8 @@ def parse(argv=None):
     ap.add_argument("--mode", default="max")
     ap.add_argument("--spec", default=False)
     ap.add_argument("--llr_device", choices=["cuda", "cpu"], default="cuda")
+    ap.add_argument("--llr_producer", choices=["fused", "ops"], default="fused",
+                    help="cuda LLRs: one fused HIP kernel (Philox; default) or the op-by-op torch port")
     ap.add_argument("--target_block_errs", type=int, default=1000)
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--plot", default=None, help="save the BLER plot here (matplotlib)")
@@ -76,7 +78,13 @@ def gen_code(c, name, mode, device, generator=None):  # main.py:32-41
         dec = SCL_Dec(fp, c.n, c.list_size, device=dev_str)
     else:
         raise Exception('error...')
-    model = channel.System_AWGN_model(c.n, c.k, enc, dec, device=device, generator=generator)
+    if device.type == "cuda" and getattr(c, "llr_producer", "fused") == "fused":
+        # one HIP launch for bits/encoder/mapper/channel/demapper; rank r draws stream rows
+        # [r*bs, (r+1)*bs) of the seed's stream
+        rank = int(os.environ.get("RANK", "0"))
+        model = channel.FusedAWGN(c.n, c.k, fp, dec, device=device, seed=c.seed, row0=rank * c.bs)
+    else:
+        model = channel.System_AWGN_model(c.n, c.k, enc, dec, device=device, generator=generator)
     return [model, name]
 
 

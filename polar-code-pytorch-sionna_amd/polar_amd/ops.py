@@ -94,3 +94,42 @@ def polar_encode(plan, u_bits, out=None):
         _lib.check(_lib.lib().pl_polar_encode(plan.handle, ctypes.c_void_p(u.data_ptr()), bs,
                                               ctypes.c_void_p(out.data_ptr()), st), "pl_polar_encode")
     return out
+
+
+def awgn_qpsk_llr(plan, bs, no, seed, iteration, row0=0, with_bits=True):
+    """The fused System_AWGN_model producer (pl_awgn_qpsk_llr) on the plan's device: returns
+    (u [bs, k] fp32 0/1 or None, logits [bs, n] fp32) for rows row0.. of the (seed, iteration)
+    stream."""
+    dev = plan.device
+    no = float(no)
+    if not no > 0.0:
+        raise ValueError(f"noise variance must be positive, got {no}")
+    llr = torch.empty((bs, plan.n), dtype=torch.float32, device=dev)
+    u = torch.empty((bs, plan.k), dtype=torch.float32, device=dev) if with_bits else None
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().pl_awgn_qpsk_llr(plan.handle, int(seed) & (2 ** 64 - 1), int(iteration) & (2 ** 64 - 1),
+                                               int(row0), int(bs), no,
+                                               ctypes.c_void_p(u.data_ptr() if u is not None else 0),
+                                               ctypes.c_void_p(llr.data_ptr()), _lib.current_stream_ptr(dev)),
+                   "pl_awgn_qpsk_llr")
+    return u, llr
+
+
+def count_errors(a, b, counts=None):
+    """[bit errors, block errors] (int64, on the device) of two [..., k] 0/1 fp32 tensors
+    (my_sn/sim.py:7-18 count_errors / count_block_errors in one pass); accumulates into counts."""
+    _require_cuda(a, "a")
+    _require_cuda(b, "b")
+    if a.shape != b.shape or a.device != b.device:
+        raise ValueError("count_errors: tensors must have the same shape and device")
+    k = a.shape[-1] if a.dim() else 1
+    x = a.to(torch.float32).contiguous()
+    y = b.to(torch.float32).contiguous()
+    rows = x.numel() // k if k else 0
+    if counts is None:
+        counts = torch.zeros(2, dtype=torch.int64, device=a.device)
+    with torch.cuda.device(a.device):
+        _lib.check(_lib.lib().pl_count_errors(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(y.data_ptr()), rows, k,
+                                              ctypes.c_void_p(counts.data_ptr()), _lib.current_stream_ptr(a.device)),
+                   "pl_count_errors")
+    return counts

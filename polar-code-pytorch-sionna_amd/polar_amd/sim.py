@@ -61,8 +61,14 @@ def sim_ber(mc_fun, ebno_dbs, batch_size, max_mc_iter, soft_estimates=False, tar
             b, b_hat = mc_fun(batch_size=batch_size, ebno_db=ebno_dbs[i])
             if soft_estimates:
                 b_hat = hard_decisions(b_hat)
-            inc = tc.stack([count_errors(b, b_hat), count_block_errors(b, b_hat),
-                            tc.tensor(b.numel(), device=b.device), tc.tensor(b.numel() // b.shape[-1], device=b.device)])
+            if b.is_cuda and b_hat.is_cuda and b.shape == b_hat.shape and b.shape[-1] > 0:
+                # both counters in one HIP pass (pl_count_errors), no torch reductions
+                from . import ops
+                be = ops.count_errors(b, b_hat)
+                inc = tc.cat([be, tc.tensor([b.numel(), b.numel() // b.shape[-1]], dtype=tc.int64, device=b.device)])
+            else:
+                inc = tc.stack([count_errors(b, b_hat), count_block_errors(b, b_hat),
+                                tc.tensor(b.numel(), device=b.device), tc.tensor(b.numel() // b.shape[-1], device=b.device)])
             inc = inc.to(cdev)
             if dist is not None:
                 dist.all_reduce(inc, op=dist.ReduceOp.SUM, group=process_group)
