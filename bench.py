@@ -102,11 +102,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # one rank per GPU; PL_BENCH_BACKEND=gloo with more ranks than GPUs is the rehearsal of the
+    # multi-GPU path on a one-GPU box (ranks share the card, gloo carries the collectives)
+    gpu = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        backend = os.environ.get("PL_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(backend)
+    dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
 
     import polar_amd
@@ -158,8 +165,9 @@ def main():
     wall = time.perf_counter() - t0
     kern_ms = e0.elapsed_time(e1) / a.steps
 
-    blk = torch.tensor([int(torch.any(out != bits, dim=-1).sum().item()), bs], dtype=torch.int64, device=dev)
-    tmax = torch.tensor([wall], dtype=torch.float64, device=dev)
+    cdev = dev if os.environ.get("PL_BENCH_BACKEND", "nccl") == "nccl" else torch.device("cpu")  # gloo: host
+    blk = torch.tensor([int(torch.any(out != bits, dim=-1).sum().item()), bs], dtype=torch.int64, device=cdev)
+    tmax = torch.tensor([wall], dtype=torch.float64, device=cdev)
     if dist is not None:
         dist.all_reduce(blk, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
