@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--list-size", type=int, default=8)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sim-iteration", action="store_true",
+                    help="skip the (untimed-region) Monte-Carlo iteration measurement of the fused producer")
     a = ap.parse_args()
     if a.bs is None:
         a.bs = 65536 if a.decoder == "sc" else 8192  # BASELINE.json configs[2] / configs[3]
@@ -83,6 +85,39 @@ def cpu_baseline(llr_host, fp, k, n, decoder, L, budget_s):
                                    "threads): 0.00603 Mcodewords/s at this shape (BASELINE.md §2)") if decoder == "sc"
             else ("reference x_run SCL_Dec (L=8) measured in the build container (8 Xeon threads): "
                   "6.15e-06 Mcodewords/s at n=1024 (BASELINE.md §2)")}
+
+
+def sim_iteration(plan, fp, k, n, bs, ebno, dev, reps=20):
+    """One Monte-Carlo iteration of the harness on this GPU, measured
+    after the timed region: the fused producer (pl_awgn_qpsk_llr: bits, encoder, QPSK, AWGN,
+    logits), the SC decode and the error counter (pl_count_errors), each by HIP events."""
+    from polar_amd import _lib, channel, ops
+    enc = _lib.Plan(n, plan_mask(fp, n), 1, flags=_lib.PL_PLAN_GENERIC, device=dev)
+    no = float(channel.ebnodb2no(ebno, 2, k / n))
+    out = torch.empty((bs, k), dtype=torch.float32, device=dev)
+    u, llr = ops.awgn_qpsk_llr(enc, bs, no, 42, 0)
+    counts = torch.zeros(2, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    t = {}
+    for name, fn in (("producer_ms", lambda: ops.awgn_qpsk_llr(enc, bs, no, 42, 1)),
+                     ("decode_ms", lambda: ops.sc_decode(plan, llr, out=out)),
+                     ("count_ms", lambda: ops.count_errors(u, out, counts=counts))):
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        t[name] = round(e0.elapsed_time(e1) / reps, 5)
+    tot = sum(t.values())
+    return {"mcw_s": round(bs / tot / 1e3, 2), **t,
+            "note": "fused producer + SC decode + error count per iteration, one GPU, HIP events"}
+
+
+def plan_mask(fp, n):
+    import polar_amd
+    return polar_amd.frozen_mask(fp, n)
 
 
 def traffic_from_profiles(tag):
@@ -177,6 +212,9 @@ def main():
     bytes_per_launch = bs * (4 * n + 4 * k)
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
     tag = f"{a.decoder}_k{k}_n{n}_bs{bs}" + (f"_L{L}" if L > 1 else "")
+    sim_it = None
+    if a.decoder == "sc" and not a.no_sim_iteration:
+        sim_it = sim_iteration(plan, fp, k, n, bs, a.ebno, dev)
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(llr.cpu().numpy(), fp.numpy(), k, n, a.decoder, L, a.cpu_seconds)
@@ -207,6 +245,8 @@ def main():
                          "kernel_ms": round(kern_ms, 5), "algorithmic_bytes_per_launch": bytes_per_launch},
             "cpu_baseline": cpu,
         }
+        if sim_it is not None:
+            line["sim_iteration"] = sim_it
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
