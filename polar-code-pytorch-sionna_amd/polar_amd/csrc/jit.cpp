@@ -307,12 +307,17 @@ int attach_static(pl_plan* p, const uint8_t* frozen, bool allow_compile) {
     if (hipModuleGetGlobal(&gp, &gsz, mod, "pl_sc_persistent") == hipSuccess && gsz == sizeof(int))
         (void)hipMemcpyDtoH(&persistent, gp, sizeof(int));
     (void)hipGetLastError();
+    int bpc = 2;  // resident blocks per CU of a persistent kernel (pl_sc_blocks_per_cu, default 2)
+    if (persistent && hipModuleGetGlobal(&gp, &gsz, mod, "pl_sc_blocks_per_cu") == hipSuccess && gsz == sizeof(int))
+        (void)hipMemcpyDtoH(&bpc, gp, sizeof(int));
+    (void)hipGetLastError();
+    if (bpc < 1) bpc = 1;
     int dev = 0, cus = 0;
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
     p->sc_log_g = lg;
     p->sc_persistent = persistent;
-    p->resident_blocks = 2 * cus;
+    p->resident_blocks = bpc * cus;
     p->sc_module = mod;
     p->sc_fn_f32 = f32;
     p->sc_fn_u8 = u8;

@@ -65,6 +65,18 @@ typedef unsigned long uintptr_t;
 #ifndef PL_SC_SPC_BALLOT
 #define PL_SC_SPC_BALLOT 0  // 1: SALU ballot uniqueness test instead of a DPP count; measured slower
 #endif
+#ifndef PL_SC_HD_SUB
+#define PL_SC_HD_SUB 1  // leaf decisions as one fp32 subtract of the smallest denormal
+#endif
+#ifndef PL_SC_VA_RECOMPUTE
+#define PL_SC_VA_RECOMPUTE 0  // 1: recompute the left virtual LLRs for the g pass (-32 VGPRs); measured slower
+#endif
+#ifndef PL_SC_WIDE
+#define PL_SC_WIDE 8  // in-lane partial sums of nodes with <= this many slots per lane: one word per slot
+#endif
+#ifndef PL_SC_PK_G
+#define PL_SC_PK_G 1  // in-lane g adds in pairs (v_pk_add_f32)
+#endif
 #ifndef PL_SC_ROOT_MODE
 #define PL_SC_ROOT_MODE 0
 #endif
@@ -190,10 +202,18 @@ __device__ __forceinline__ uint32_t bit31(W w, int j) {
 }
 // hard decision of a leaf, u = 1 iff !(llr > 0) (polar_sc.py:94-97), as a bit-31 flag.
 // PL_SC_LANE31: only bit 31 of a lane-level flag is meaningful (its consumers mask with the
-// lo31/hi31 lane masks or shift by 31), so the decision is one saturating subtract on the bit
-// pattern: bits(x) - 1 is negative iff bits(x) <= 0 as a signed integer, i.e. x <= +0 or x < 0
-// (no NaN), and the saturation keeps -0 (INT_MIN) negative.  No compare, no VCC.
-#if PL_SC_LANE31
+// lo31/hi31 lane masks or shift by 31), so the decision is one arithmetic op, no compare, no VCC.
+// PL_SC_HD_SUB=0 form: one saturating subtract on the bit pattern -- bits(x) - 1 is negative iff
+// bits(x) <= 0 as a signed integer, i.e. x <= +0 or x < 0 (no NaN), and the saturation keeps -0
+// (INT_MIN) negative.  The default form is a plain fp32 subtract, which issues faster on gfx950
+// (tools/micro/issue_cost*.hip: v_add_f32 ~1.1 ns, v_add_i32 clamp ~1.8 ns per wave-instruction).
+#if PL_SC_LANE31 && PL_SC_HD_SUB
+// x - 2^-149 (the smallest denormal) is negative exactly when x <= 0: +0 and -0 give -2^-149,
+// x = 2^-149 gives +0 (an exact zero rounds to +0), larger x stay positive.  Needs fp32 denormals
+// preserved, which both build paths keep (no FTZ flag: .amdhsa_float_denorm_mode_32 3); the
+// exact-zero golden sets would catch a flushing build.
+__device__ __forceinline__ uint32_t hd31(float x) { return fu(x - 1.40129846e-45f); }
+#elif PL_SC_LANE31
 __device__ __forceinline__ uint32_t hd31(float x) {
     return (uint32_t)__builtin_elementwise_sub_sat((int32_t)fu(x), (int32_t)1);
 }
@@ -265,9 +285,10 @@ __device__ __forceinline__ uint32_t lsplit(float a, const Lane& ln) {
     if constexpr (nt<C>(s - 1, P) != R0) bl = lnode<C, s - 1, P>(fop<C::FM, lchild<C>(s, P)>(a, y, ln.lmax), ln);
 #if PL_SC_LANE31
     // both lanes of the pair evaluate (1-2u) alpha_lo + alpha_hi: the low lane flips its own
-    // value, the high lane its partner's (bitop3 S1 ^ (S0 & S2) with the lane's bit-31 mask)
-    const float x = uf(__builtin_amdgcn_bitop3_b32(bl, fu(a), ln.lo31[s], 0x6c)) +
-                    uf(__builtin_amdgcn_bitop3_b32(bl, fu(y), ln.hi31[s], 0x6c));
+    // value (bitop3 S1 ^ (S0 & S2) with the lane's bit-31 mask), the high lane keeps its own, and
+    // one DPP add sums the pair in both lanes (fp32 addition is commutative: same bits)
+    const float v = uf(__builtin_amdgcn_bitop3_b32(bl, fu(a), ln.lo31[s], 0x6c));
+    const float x = v + mirf<S>(v);
     const uint32_t br = lnode<C, s - 1, P + S / 2>(x, ln);
     return __builtin_amdgcn_bitop3_b32(bl, br, ln.lo31[s], 0x6c);  // br ^ (bl & lo31)
 #else
@@ -334,40 +355,125 @@ __device__ __forceinline__ uint32_t lnode(float a, const Lane& ln) {
 }
 
 // ---------------- in-lane nodes: size 2^s >= 2G, E = 2^s / G slots per lane ---------------
-template <class C, int s, int P>
-__device__ Beta<(1 << s) / C::G> node(const float (&a)[(1 << s) / C::G], const Lane& ln);
+// Partial sums of a node with E <= PL_SC_WIDE slots per lane are kept "wide": one word per slot
+// whose bit 31 is the bit (lower bits are don't-care), so g applies a flag with one bitop3 and the
+// combine [bl ^ br, br] is E/2 XORs -- no bit extraction (v_lshlrev) per g element.  Larger nodes
+// keep packed words (bit j = slot j), which bounds the registers of the long-lived upper stages.
+template <int E>
+struct Wide {
+    uint32_t w[E];
+};
+template <int E>
+using BV = typename Cond<(E <= PL_SC_WIDE), Wide<E>, Beta<E>>::type;
+
+template <int E>
+__device__ __forceinline__ uint32_t flag(const Wide<E>& b, int j) { return b.w[j]; }
+__device__ __forceinline__ uint32_t flag(uint32_t b, int j) { return bit31(b, j); }
+__device__ __forceinline__ uint32_t flag(uint64_t b, int j) { return bit31(b, j); }
+
+template <int E>
+__device__ __forceinline__ BV<E> bzero() {
+    BV<E> r;
+    if constexpr (E <= PL_SC_WIDE) {
+#pragma unroll
+        for (int j = 0; j < E; ++j) r.w[j] = 0u;
+    } else {
+        r = 0;
+    }
+    return r;
+}
+// packed words of a wide partial-sum vector: bit j = bit 31 of word j.  One v_alignbit per bit:
+// alignbit(acc, w, 31) = (acc << 1) | (w >> 31), inserting from the top slot down.
+template <int E>
+__device__ __forceinline__ Beta<E> packed(const Wide<E>& b) {
+    Beta<E> r = 0;
+    if constexpr (E <= 32) {
+        uint32_t acc = b.w[E - 1] >> 31;
+#pragma unroll
+        for (int j = E - 2; j >= 0; --j) acc = __builtin_amdgcn_alignbit(acc, b.w[j], 31);
+        r = acc;
+    } else {
+        uint32_t lo = b.w[31] >> 31, hi = b.w[E - 1] >> 31;
+#pragma unroll
+        for (int j = 30; j >= 0; --j) lo = __builtin_amdgcn_alignbit(lo, b.w[j], 31);
+#pragma unroll
+        for (int j = E - 2; j >= 32; --j) hi = __builtin_amdgcn_alignbit(hi, b.w[j], 31);
+        r = ((uint64_t)hi << 32) | lo;
+    }
+    return r;
+}
+__device__ __forceinline__ uint32_t packed(uint32_t b) { return b; }
+__device__ __forceinline__ uint64_t packed(uint64_t b) { return b; }
+
+// [bl ^ br, br] (polar_sc.py:83-89)
+template <int H>
+__device__ __forceinline__ BV<2 * H> combine(const BV<H>& bl, const BV<H>& br) {
+    BV<2 * H> r;
+    if constexpr (2 * H <= PL_SC_WIDE) {
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            r.w[j] = bl.w[j] ^ br.w[j];
+            r.w[j + H] = br.w[j];
+        }
+    } else {
+        using BT = Beta<2 * H>;
+        const Beta<H> pl = packed(bl), pr = packed(br);
+        r = (BT)(pl ^ pr) | ((BT)pr << H);
+    }
+    return r;
+}
 
 template <class C, int s, int P>
-__device__ __forceinline__ Beta<(1 << (s - 1)) / C::G> child(const float (&x)[(1 << (s - 1)) / C::G],
-                                                             const Lane& ln) {
+__device__ BV<(1 << s) / C::G> node(const float (&a)[(1 << s) / C::G], const Lane& ln);
+
+template <class C, int s, int P>
+__device__ __forceinline__ BV<(1 << (s - 1)) / C::G> child(const float (&x)[(1 << (s - 1)) / C::G], const Lane& ln) {
     if constexpr ((1 << (s - 1)) == C::G) {
+#if PL_SC_WIDE >= 1
+        return Wide<1>{{lnode<C, s - 1, P>(x[0], ln)}};
+#else
         return (Beta<1>)(lnode<C, s - 1, P>(x[0], ln) >> 31);
+#endif
     } else {
         return node<C, s - 1, P>(x, ln);
     }
 }
 
+typedef float f2v __attribute__((ext_vector_type(2)));
+// x[j] = g(a[j], a[j + H], flag j of bl) for j < H (polar_sc.py:49-53), two adds per v_pk_add_f32
+template <int H, typename B>
+__device__ __forceinline__ void gvec(const float (&a)[2 * H], const B& bl, float (&x)[H]) {
+    if constexpr (H >= 2 && PL_SC_PK_G) {
+#pragma unroll
+        for (int j = 0; j < H; j += 2) {
+            const f2v u = {flip31(a[j], flag(bl, j)), flip31(a[j + 1], flag(bl, j + 1))};
+            const f2v w = {a[j + H], a[j + 1 + H]};
+            const f2v r = u + w;
+            x[j] = r.x;
+            x[j + 1] = r.y;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < H; ++j) x[j] = gop(a[j], a[j + H], flag(bl, j));
+    }
+}
+
 template <class C, int s, int P>
-__device__ __forceinline__ Beta<(1 << s) / C::G> split(const float (&a)[(1 << s) / C::G], const Lane& ln) {
+__device__ __forceinline__ BV<(1 << s) / C::G> split(const float (&a)[(1 << s) / C::G], const Lane& ln) {
     constexpr int E = (1 << s) / C::G, H = E / 2, h = 1 << (s - 1);
-    using BH = Beta<H>;
-    using BT = Beta<E>;
     float x[H];
-    BH bl = 0;
+    BV<H> bl = bzero<H>();
     if constexpr (nt<C>(s - 1, P) != R0) {
 #pragma unroll
         for (int j = 0; j < H; ++j) x[j] = fop<C::FM, lchild<C>(s, P)>(a[j], a[j + H], ln.lmax);
         bl = child<C, s, P>(x, ln);
-#pragma unroll
-        for (int j = 0; j < H; ++j) {
-            x[j] = gop(a[j], a[j + H], bit31(bl, j));
-        }
+        gvec<H>(a, bl, x);
     } else {
 #pragma unroll
         for (int j = 0; j < H; ++j) x[j] = a[j] + a[j + H];
     }
-    const BH br = child<C, s, P + h>(x, ln);
-    return (BT)(bl ^ br) | ((BT)br << H);
+    const BV<H> br = child<C, s, P + h>(x, ln);
+    return combine<H>(bl, br);
 }
 
 template <class C, int E>
@@ -377,17 +483,29 @@ __device__ __forceinline__ Beta<E> signs(const float (&a)[E]) {
     for (int j = 0; j < E; ++j) b |= (Beta<E>)(fu(a[j]) >> 31) << j;
     return b;
 }
+template <int E>
+__device__ __forceinline__ BV<E> from_packed(Beta<E> b) {
+    if constexpr (E <= PL_SC_WIDE) {
+        Wide<E> r;
+#pragma unroll
+        for (int j = 0; j < E; ++j) r.w[j] = bit31(b, j);
+        return r;
+    } else {
+        return b;
+    }
+}
 
 template <class C, int s, int P>
-__device__ __forceinline__ Beta<(1 << s) / C::G> node(const float (&a)[(1 << s) / C::G], const Lane& ln) {
+__device__ __forceinline__ BV<(1 << s) / C::G> node(const float (&a)[(1 << s) / C::G], const Lane& ln) {
     constexpr int E = (1 << s) / C::G;
     constexpr int T = nt<C>(s, P);
     using BT = Beta<E>;
+    constexpr bool WIDE = E <= PL_SC_WIDE;
 #if PL_SC_DIAG_SKIP_SPECIAL
-    if constexpr (T == REP || T == SPC || T == R1) return signs<C, E>(a);  // diagnostic only
+    if constexpr (T == REP || T == SPC || T == R1) return from_packed<E>(signs<C, E>(a));  // diagnostic only
 #endif
     if constexpr (T == R0) {
-        return (BT)0;
+        return bzero<E>();
     } else if constexpr (T == REP) {
         float y[E];
 #pragma unroll
@@ -397,12 +515,29 @@ __device__ __forceinline__ Beta<(1 << s) / C::G> node(const float (&a)[(1 << s) 
 #pragma unroll
             for (int j = 0; j < hh; ++j) y[j] = y[j] + y[j + hh];
         const float v = grp_sumf<C::LOG_G>(y[0]);
-        return hd(v) ? ones<E>() : (BT)0;
+        if constexpr (WIDE) {
+            Wide<E> r;
+            const uint32_t u = hd31(v);
+#pragma unroll
+            for (int j = 0; j < E; ++j) r.w[j] = u;
+            return r;
+        } else {
+            return hd(v) ? ones<E>() : (BT)0;
+        }
     } else if constexpr (T == R1 && C::FM == 0) {
         bool z = false;
 #pragma unroll
         for (int j = 0; j < E; ++j) z |= (a[j] == 0.0f);
-        if (!any_lane(z)) return signs<C, E>(a);
+        if (!any_lane(z)) {
+            if constexpr (WIDE) {
+                Wide<E> r;
+#pragma unroll
+                for (int j = 0; j < E; ++j) r.w[j] = fu(a[j]);  // bit 31 = the decision
+                return r;
+            } else {
+                return signs<C, E>(a);
+            }
+        }
         return split<C, s, P>(a, ln);
     } else if constexpr (T == SPC && C::FM == 0) {
         bool z = false;
@@ -428,7 +563,7 @@ __device__ __forceinline__ Beta<(1 << s) / C::G> node(const float (&a)[(1 << s) 
         cnt = grp<C::LOG_G>(cnt, [](uint32_t u, uint32_t v) { return u + v; });
         const bool bad = any_lane(z | ((par != 0u) & ((cnt != 1u) | (mn >= fu(ln.lmax)))));
 #endif
-        if (!bad) return par ? (BT)(b ^ eqm) : b;
+        if (!bad) return from_packed<E>(par ? (BT)(b ^ eqm) : b);
         return split<C, s, P>(a, ln);
     } else {
         return split<C, s, P>(a, ln);
@@ -446,6 +581,25 @@ template <class C>
 __device__ __forceinline__ float valpha(const float (&ch)[C::NS], int side, uint64_t blr, int j, float lmax) {
     const float x = ch[j], y = ch[j + C::NS / 2];
     return side == 0 ? fop<C::FM>(x, y, lmax) : (-flip31(x, bit31(blr, j))) - y;
+}
+
+// all NS/2 virtual stage-(LOG_N-1) LLRs of one half
+template <class C, int SIDE>
+__device__ __forceinline__ void valphas(const float (&ch)[C::NS], uint64_t blr, float (&a)[C::NS / 2], float lmax) {
+    constexpr int E = C::NS / 2;
+    if constexpr (SIDE == 1 && E >= 2) {
+#pragma unroll
+        for (int j = 0; j < E; j += 2) {
+            const f2v u = {flip31(ch[j], bit31(blr, j)), flip31(ch[j + 1], bit31(blr, j + 1))};
+            const f2v w = {ch[j + E], ch[j + 1 + E]};
+            const f2v r = -u - w;
+            a[j] = r.x;
+            a[j + 1] = r.y;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < E; ++j) a[j] = valpha<C>(ch, SIDE, blr, j, lmax);
+    }
 }
 
 struct NoHook {
@@ -470,29 +624,33 @@ __device__ __forceinline__ Beta<C::NS / 2> half(float (&ch)[C::NS], uint64_t blr
         return (BT)(lnode<C, s, P>(a, ln) >> 31);
     } else if constexpr (T != GEN) {
         float a[E];
-#pragma unroll
-        for (int j = 0; j < E; ++j) a[j] = valpha<C>(ch, SIDE, blr, j, ln.lmax);
+        valphas<C, SIDE>(ch, blr, a, ln.lmax);
         after();
-        return node<C, s, P>(a, ln);
+        return packed(node<C, s, P>(a, ln));
     } else {
         constexpr int H = E / 2, h = 1 << (s - 1);
-        using BH = Beta<H>;
+        using BH = BV<H>;
         float x[H];
-        BH bl = 0;
+        BH bl = bzero<H>();
+        float va[E];
+        valphas<C, SIDE>(ch, blr, va, ln.lmax);
         if constexpr (nt<C>(s - 1, P) != R0) {
 #pragma unroll
-            for (int j = 0; j < H; ++j)
-                x[j] = fop<C::FM, SIDE == 0>(valpha<C>(ch, SIDE, blr, j, ln.lmax),
-                                             valpha<C>(ch, SIDE, blr, j + H, ln.lmax), ln.lmax);
+            for (int j = 0; j < H; ++j) x[j] = fop<C::FM, SIDE == 0>(va[j], va[j + H], ln.lmax);
             bl = child<C, s, P>(x, ln);
-        }
+#if PL_SC_VA_RECOMPUTE
+            // recompute the virtual LLRs for the g pass instead of keeping them live across the
+            // left subtree (32 VGPRs at n = 1024): the opaque copy keeps the compiler from reusing
+            // the f-pass values
 #pragma unroll
-        for (int j = 0; j < H; ++j)
-            x[j] = gop(valpha<C>(ch, SIDE, blr, j, ln.lmax), valpha<C>(ch, SIDE, blr, j + H, ln.lmax),
-                       bit31(bl, j));
+            for (int j = 0; j < C::NS; ++j) asm volatile("" : "+v"(ch[j]));
+            valphas<C, SIDE>(ch, blr, va, ln.lmax);
+#endif
+        }
+        gvec<H>(va, bl, x);
         after();
         const BH br = child<C, s, P + h>(x, ln);
-        return (BT)(bl ^ br) | ((BT)br << H);
+        return packed(combine<H>(bl, br));
     }
 }
 
@@ -810,7 +968,7 @@ __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs
 #pragma unroll
             for (int j = 0; j < E; ++j) a[j] = fop<C::FM>(ch[j * G + res], ch[(j + E) * G + res], lmax);
             if constexpr (E == 1) bl = lnode<C, C::LOG_N - 1, 0>(a[0], ln) >> 31;
-            else bl = node<C, C::LOG_N - 1, 0>(a, ln);
+            else bl = packed(node<C, C::LOG_N - 1, 0>(a, ln));
         }
         {
             const float* chp = ch;
@@ -820,7 +978,7 @@ __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs
             for (int j = 0; j < E; ++j)
                 a[j] = (-flip31(chp[j * G + res], bit31(bl, j))) - chp[(j + E) * G + res];
             if constexpr (E == 1) br = lnode<C, C::LOG_N - 1, N / 2>(a[0], ln) >> 31;
-            else br = node<C, C::LOG_N - 1, N / 2>(a, ln);
+            else br = packed(node<C, C::LOG_N - 1, N / 2>(a, ln));
         }
         if constexpr (NS / 2 >= 64) {
             lo = (uint64_t)(bl ^ br);
@@ -983,8 +1141,12 @@ __device__ __forceinline__ void decode_staged(const float* __restrict__ llr, int
         pls::decode<CODE, OUTK>(llr, bs, out, info_loc, k, lmax, ulds);                                      \
     }
 #endif
+#ifndef PL_SC_PERSIST_BPC
+#define PL_SC_PERSIST_BPC 2  // resident blocks per CU the launcher gives a persistent kernel
+#endif
 #define PL_SC_STATIC_KERNELS(CODE)                                                                           \
     extern "C" __device__ const int pl_sc_persistent = PL_SC_PERSIST;                                       \
+    extern "C" __device__ const int pl_sc_blocks_per_cu = PL_SC_PERSIST_BPC;                                \
     PL_SC_ENTRY(CODE, pl_sc_static_f32, pls::OUT_F32)                                                        \
     PL_SC_ENTRY(CODE, pl_sc_static_u8, pls::OUT_U8)
 
