@@ -136,6 +136,30 @@ def test_random_codes():
     return out
 
 
+ROOT_HALF_PAIRS = [("R0", "GEN"), ("GEN", "R0"), ("R0", "R1"), ("R1", "R0"), ("REP", "SPC"), ("SPC", "REP"),
+                   ("GEN", "R1"), ("R1", "GEN"), ("REP", "GEN"), ("GEN", "SPC")]
+
+
+def root_half_codes():
+    """n = 1024 frozen masks whose two root halves are each rate-0, rate-1, repetition, SPC or the
+    reference (512,1024) code's half (tests/test_sc_gpu.py::test_sc_root_half_types): every branch
+    of the specialised kernel's virtual root, including the LDS channel half (sc_static.h Ch)."""
+    import numpy as np
+    data = os.path.join(HERE, "data", "frozen_sets.npz")
+    with np.load(data) as d:
+        ref = np.zeros(1024, dtype=np.uint8)
+        ref[d["k512_n1024"].astype(np.int64)] = 1
+    h = 512
+    kinds = {"R0": np.ones(h, np.uint8), "R1": np.zeros(h, np.uint8),
+             "REP": np.r_[np.ones(h - 1, np.uint8), 0], "SPC": np.r_[1, np.zeros(h - 1, np.uint8)]}
+    out = []
+    for a, b in ROOT_HALF_PAIRS:
+        left = ref[:h] if a == "GEN" else kinds[a]
+        right = ref[h:] if b == "GEN" else kinds[b]
+        out.append((a + "_" + b, np.concatenate([left, right]).astype(np.uint8)))
+    return out
+
+
 # 5G NR (k, E) configurations the package's tests decode (tests/test_polar5g_gpu.py); their
 # mother codes are decoded by the exact-f SC kernel (Polar5GDecoder dec_type="SC")
 POLAR5G_TEST_CODES = [(12, 20), (12, 160), (16, 64), (19, 100), (20, 40), (24, 300), (32, 64), (40, 100), (48, 64),
@@ -179,6 +203,7 @@ def reference_codes():
     with contextlib.redirect_stdout(io.StringIO()):  # the CRC6 warning of 12 <= k <= 19
         out += polar5g_codes()
     out += test_random_codes()
+    out += [(m, 0) for _, m in root_half_codes()]
     uniq = {}
     for m, fm in out:
         uniq[(bytes(bytearray(m)), fm)] = (m, fm)

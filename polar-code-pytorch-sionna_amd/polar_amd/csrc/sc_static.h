@@ -71,6 +71,9 @@ typedef unsigned long uintptr_t;
 #ifndef PL_SC_VA_RECOMPUTE
 #define PL_SC_VA_RECOMPUTE 0  // 1: recompute the left virtual LLRs for the g pass (-32 VGPRs); measured slower
 #endif
+#ifndef PL_SC_CH_LDS
+#define PL_SC_CH_LDS 1  // the upper half of the channel slots lives in LDS (LDS-DMA), not VGPRs (see Ch)
+#endif
 #ifndef PL_SC_WIDE
 #define PL_SC_WIDE 8  // in-lane partial sums of nodes with <= this many slots per lane: one word per slot
 #endif
@@ -122,6 +125,16 @@ struct Cond<false, T, F> {
 };
 template <int E>
 using Beta = typename Cond<(E <= 32), uint32_t, uint64_t>::type;
+
+// PL_SC_CH_LDS applies to n = 1024 at 16 lanes per codeword (64 channel slots per lane): 8 KiB of
+// LDS per wave, 32 KiB per block, so four blocks fit a CU's 160 KiB, and the 32 VGPRs saved
+// (133 -> 103) lift the kernel from three to four waves per SIMD: 0.0854 vs 0.0882 ms at
+// (512,1024), bs = 65536 (profiles/r02s_sc_ab_ch_lds.txt).  At n = 64 ... 512 the kernel already
+// ran at that occupancy and the LDS round trip only costs (+4 ... +39 %), so they keep VGPRs.
+template <class C>
+struct Ch {
+    static constexpr int CHL = (PL_SC_CH_LDS && C::NS == 64 && C::LOG_N == 10) ? 1 : 0;
+};
 
 template <class C>
 constexpr int nt(int s, int p) {
@@ -202,7 +215,7 @@ __device__ __forceinline__ uint32_t bit31(W w, int j) {
 }
 // hard decision of a leaf, u = 1 iff !(llr > 0) (polar_sc.py:94-97), as a bit-31 flag.
 // PL_SC_LANE31: only bit 31 of a lane-level flag is meaningful (its consumers mask with the
-// lo31/hi31 lane masks or shift by 31), so the decision is one arithmetic op, no compare, no VCC.
+// lo31 lane masks or shift by 31), so the decision is one arithmetic op, no compare, no VCC.
 // PL_SC_HD_SUB=0 form: one saturating subtract on the bit pattern -- bits(x) - 1 is negative iff
 // bits(x) <= 0 as a signed integer, i.e. x <= +0 or x < 0 (no NaN), and the saturation keeps -0
 // (INT_MIN) negative.  The default form is a plain fp32 subtract, which issues faster on gfx950
@@ -229,15 +242,16 @@ __device__ __forceinline__ uint64_t ballot_lanes(bool p) { return __builtin_amdg
 
 struct Lane {
 #if PL_SC_LANE31
-    // lo31[t] / hi31[t]: 0x80000000 if this lane holds the low / high element of its pair at
+    // lo31[t]: 0x80000000 if this lane holds the low element of its pair at
     // level 2^t, else 0 (bitop3 operands; opaque to the compiler, see decode())
-    uint32_t lo31[5], hi31[5];
+    uint32_t lo31[5];
     __device__ __forceinline__ uint32_t lom(int t) const { return (uint32_t)((int32_t)lo31[t] >> 31); }
 #else
     uint32_t lom_[5];  // lom[t]: all-ones if this lane holds the low element at level 2^t
     __device__ __forceinline__ uint32_t lom(int t) const { return lom_[t]; }
 #endif
     float lmax;
+    const float* chl;  // PL_SC_CH_LDS: this lane's first LDS channel word (slot NS/2), stride 64 words
 };
 
 // ---------------- reductions over the G lanes of a codeword (all lanes get the result) ----
@@ -615,6 +629,15 @@ __device__ __forceinline__ Beta<C::NS / 2> half(float (&ch)[C::NS], uint64_t blr
     constexpr int E = C::NS / 2;  // slots of the stage-(LOG_N-1) node per lane
     using BT = Beta<E>;
     constexpr int T = nt<C>(s, P);
+    if constexpr (Ch<C>::CHL && T != R0) {
+        // the upper channel slots, from LDS: live only while this half's virtual LLRs are formed
+        // wait for the LDS-DMA (SIDE 1 too: a rate-0 left half reads nothing, and otherwise nothing
+        // is outstanding); the memory clobber also keeps the compiler from merging SIDE 1's reads
+        // with SIDE 0's, which would hold the values live across the whole left half
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int j = C::NS / 2; j < C::NS; ++j) ch[j] = ln.chl[(j - C::NS / 2) * 64];
+    }
     if constexpr (T == R0) {
         after();
         return (BT)0;
@@ -824,11 +847,23 @@ __device__ __forceinline__ void wave_lds_fence() {
 
 template <class C>
 __device__ __forceinline__ void load_channel(float (&chv)[C::NS], const float* __restrict__ llr, int64_t cw0,
-                                             int64_t bs, int lane, int res) {
+                                             int64_t bs, int lane, int res, float* chl_wave = nullptr) {
     const int64_t cw = cw0 + (lane >> C::LOG_G);
     const float* ch = llr + (size_t)(cw < bs ? cw : bs - 1) * C::N;
+    if constexpr (Ch<C>::CHL) {
+        // slots [0, NS/2) into VGPRs; slots [NS/2, NS) by LDS-DMA, one 256-byte LDS row per slot
+        // (lane l's word at l * 4), so no VGPR holds them while the left half is decoded
 #pragma unroll
-    for (int j = 0; j < C::NS; ++j) chv[j] = ch[j * C::G + res];
+        for (int j = 0; j < C::NS / 2; ++j) chv[j] = ch[j * C::G + res];
+#pragma unroll
+        for (int j = C::NS / 2; j < C::NS; ++j)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ch + j * C::G + res),
+                                             (__attribute__((address_space(3))) void*)(chl_wave + (j - C::NS / 2) * 64),
+                                             4, 0, 0);
+    } else {
+#pragma unroll
+        for (int j = 0; j < C::NS; ++j) chv[j] = ch[j * C::G + res];
+    }
 }
 
 // Hook for half<1>: reload the channel registers with the next batch once they are dead.
@@ -882,10 +917,9 @@ __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs
 #pragma unroll
         for (int t = 0; t < 5; ++t) {
             ln.lo31[t] = t ? lom[t] & 0x80000000u : 0u;
-            ln.hi31[t] = t ? ~lom[t] & 0x80000000u : 0u;
             // keep them VGPR values: a mask the compiler knows to be 0/~0 per lane becomes an
             // SGPR lane mask and each combine a v_cndmask + v_xor instead of one v_bitop3
-            asm volatile("" : "+v"(ln.lo31[t]), "+v"(ln.hi31[t]));
+            asm volatile("" : "+v"(ln.lo31[t]));
         }
     }
 #else
@@ -893,8 +927,14 @@ __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs
     ln.lom_[0] = 0u;
 #endif
     ln.lmax = lmax;
-    uint32_t* ubase = ulds + wave * 64 * WPL;
-    uint32_t* mine = ulds + (wave * 64 + lane) * WPL;
+    // PL_SC_CH_LDS: each wave's LDS is its channel rows; its u words reuse their first 64 * WPL
+    // words once the right half has read them (same wave, LDS in order)
+    constexpr int WLDS = Ch<C>::CHL ? (NS / 2) * 64 : 64 * WPL;  // LDS words per wave
+    uint32_t* ubase = ulds + wave * WLDS;
+    uint32_t* mine = ubase + lane * WPL;
+    float* chl_wave = reinterpret_cast<float*>(ulds + wave * WLDS);
+    ln.chl = chl_wave + lane;
+    static_assert(!Ch<C>::CHL || (!PL_SC_PERSIST && PL_SC_ROOT_MODE == 0 && NS / 2 >= WPL), "PL_SC_CH_LDS: plain decoder only");
 
 #if PL_SC_PERSIST
     // Persistent, software-pipelined: each wave walks batches of CW codewords with a stride of
@@ -933,7 +973,7 @@ __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs
     for (int j = 0; j < NS; ++j) chv[j] = (float)((lane * 7 + j * 13) % 61) - 30.5f;
     asm volatile("" ::"v"(llr));
 #else
-    load_channel<C>(chv, llr, cw0, bs, lane, res);
+    load_channel<C>(chv, llr, cw0, bs, lane, res, chl_wave);
 #endif
 #if PL_SC_STAMPS
     __builtin_amdgcn_s_waitcnt(0);
@@ -1073,8 +1113,7 @@ __device__ __forceinline__ void decode_staged(const float* __restrict__ llr, int
 #pragma unroll
         for (int t = 0; t < 5; ++t) {
             ln.lo31[t] = t ? lom[t] & 0x80000000u : 0u;
-            ln.hi31[t] = t ? ~lom[t] & 0x80000000u : 0u;
-            asm volatile("" : "+v"(ln.lo31[t]), "+v"(ln.hi31[t]));
+            asm volatile("" : "+v"(ln.lo31[t]));
         }
     }
 #else
@@ -1137,7 +1176,8 @@ __device__ __forceinline__ void decode_staged(const float* __restrict__ llr, int
     extern "C" __global__ __launch_bounds__(64 * pls::kWaves, PL_SC_MINW) void NAME(                         \
         const float* __restrict__ llr, int64_t bs, void* __restrict__ out, const int32_t* __restrict__ info_loc, \
         int k, float lmax) {                                                                                  \
-        __shared__ uint32_t ulds[pls::kWaves * 64 * ((CODE::NS + 31) / 32)];                                 \
+        __shared__ uint32_t ulds[pls::Ch<CODE>::CHL ? pls::kWaves * 64 * (CODE::NS / 2)                       \
+                                                    : pls::kWaves * 64 * ((CODE::NS + 31) / 32)];              \
         pls::decode<CODE, OUTK>(llr, bs, out, info_loc, k, lmax, ulds);                                      \
     }
 #endif

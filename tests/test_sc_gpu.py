@@ -97,6 +97,26 @@ def test_sc_reference_frozen_all_shapes(pa, kind):
         assert np.array_equal(got, oracle.sc_decode(t, fp)), key
 
 
+@pytest.mark.parametrize("kind", KINDS)
+def test_sc_root_half_types(pa, kind):
+    """n = 1024 codes whose root halves are rate-0 / rate-1 / repetition / SPC / a general node:
+    every branch of the virtual root (and of the LDS channel half, sc_static.h Ch).  Pre-built by
+    build() (polar_amd.build.root_half_codes), so the specialised kernels never compile here."""
+    from polar_amd import _lib, build
+    rng = np.random.default_rng(11)
+    llr = (rng.standard_normal((257, 1024)) * 2.5).astype(np.float32)
+    llr[:, ::9] = np.round(llr[:, ::9])  # exact zeros and ties
+    llr[:5] *= 40.0  # saturation
+    x = torch.from_numpy(llr).cuda()
+    for name, m in build.root_half_codes():
+        fp = np.nonzero(m)[0]
+        flags = _lib.PL_PLAN_GENERIC if kind == "generic" else _lib.PL_PLAN_CACHE_ONLY
+        plan = _lib.Plan(1024, m, 1, 0, flags=flags)
+        assert plan.kernel()[0] == kind, (name, plan.kernel())
+        got = pa.ops.sc_decode(plan, x).cpu().numpy()
+        assert np.array_equal(got, oracle.sc_decode(llr, fp)), name
+
+
 def test_sc_full_batch_roundtrip_and_sample(pa):
     """(512,1024) at the bench batch: size-independent property + oracle on a sample."""
     fp = pa.reference_frozen_pos(512, 1024).numpy()
