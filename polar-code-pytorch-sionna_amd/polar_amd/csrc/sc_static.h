@@ -74,8 +74,11 @@ typedef unsigned long uintptr_t;
 #ifndef PL_SC_CH_LDS
 #define PL_SC_CH_LDS 1  // the upper half of the channel slots lives in LDS (LDS-DMA), not VGPRs (see Ch)
 #endif
+#ifndef PL_SC_DMA_ASM
+#define PL_SC_DMA_ASM 1  // LDS-DMA of the channel half in the saddr form (inline asm)
+#endif
 #ifndef PL_SC_WIDE
-#define PL_SC_WIDE 8  // in-lane partial sums of nodes with <= this many slots per lane: one word per slot
+#define PL_SC_WIDE 16  // in-lane partial sums of nodes with <= this many slots per lane: one word per slot
 #endif
 #ifndef PL_SC_PK_G
 #define PL_SC_PK_G 1  // in-lane g adds in pairs (v_pk_add_f32)
@@ -855,11 +858,31 @@ __device__ __forceinline__ void load_channel(float (&chv)[C::NS], const float* _
         // (lane l's word at l * 4), so no VGPR holds them while the left half is decoded
 #pragma unroll
         for (int j = 0; j < C::NS / 2; ++j) chv[j] = ch[j * C::G + res];
+#if PL_SC_DMA_ASM
+        // saddr form: wave-uniform row base in an SGPR pair (slot offset j * 64 B as the 12-bit
+        // immediate would also move the LDS address, so the base steps in SALU), this lane's
+        // 32-bit byte offset in a VGPR; M0 = the slot's LDS row.  No VALU per instruction.  The
+        // compiler does not track these loads: the reader waits with s_waitcnt vmcnt(0) (half()).
+        // base row: the wave's lowest (clamped) row, so every lane's offset is >= 0 and < 16 KiB
+        const int64_t row0 = cw0 < bs ? cw0 : bs - 1;
+        const uint32_t voff = (uint32_t)(((ch - llr) - row0 * C::N + res) * 4);
+        const uint64_t sbase = (uint64_t)(uintptr_t)(llr + row0 * C::N);
+        const uint32_t lbase = (uint32_t)(uintptr_t)chl_wave;  // LDS offset (low word of the flat address)
+#pragma unroll
+        for (int j = C::NS / 2; j < C::NS; ++j) {
+            const uint64_t a = sbase + (uint64_t)(j * C::G * 4);
+            const uint64_t sb = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a) |
+                                ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32);
+            const uint32_t lb = (uint32_t)__builtin_amdgcn_readfirstlane((int)(lbase + (j - C::NS / 2) * 256));
+            asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dword %0, %1" ::"v"(voff), "s"(sb), "s"(lb) : "memory", "m0");
+        }
+#else
 #pragma unroll
         for (int j = C::NS / 2; j < C::NS; ++j)
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ch + j * C::G + res),
                                              (__attribute__((address_space(3))) void*)(chl_wave + (j - C::NS / 2) * 64),
                                              4, 0, 0);
+#endif
     } else {
 #pragma unroll
         for (int j = 0; j < C::NS; ++j) chv[j] = ch[j * C::G + res];
