@@ -77,6 +77,9 @@ typedef unsigned long uintptr_t;
 #ifndef PL_SC_DMA_ASM
 #define PL_SC_DMA_ASM 1  // LDS-DMA of the channel half in the saddr form (inline asm)
 #endif
+#ifndef PL_SC_NT
+#define PL_SC_NT 2  // non-temporal hints: bit 0 channel loads, bit 1 output stores (see st_out4)
+#endif
 #ifndef PL_SC_WIDE
 #define PL_SC_WIDE 16  // in-lane partial sums of nodes with <= this many slots per lane: one word per slot
 #endif
@@ -157,6 +160,28 @@ __device__ __forceinline__ Beta<E> ones() {
 
 __device__ __forceinline__ uint32_t fu(float x) { return __float_as_uint(x); }
 __device__ __forceinline__ float uf(uint32_t x) { return __uint_as_float(x); }
+
+// Output rows are written once: with the non-temporal hint (PL_SC_NT bit 1) they do not push
+// the channel rows out of L2 / the Infinity Cache.  Measured with every launch streaming a batch
+// the Infinity Cache does not hold (sc_ab.py --rotate 3): 0.0809 vs 0.0841 ms; non-temporal channel
+// loads (bit 0) were slower here (0.0875 ms) although a load/store-only kernel of the same shapes
+// gains with both hints (5.78 vs 5.38 TB/s, tools/micro/load_pattern.hip).
+__device__ __forceinline__ float ld_ch(const float* p) {
+#if PL_SC_NT & 1
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_out4(float* p, float4 v) {
+#if PL_SC_NT & 2
+    const f4v w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<f4v*>(p));
+#else
+    *reinterpret_cast<float4*>(p) = v;
+#endif
+}
 
 // Mirror inside aligned blocks of S lanes: lane q reads lane q ^ (S-1).  One DPP op.
 template <int S>
@@ -783,7 +808,7 @@ __device__ __forceinline__ void emit(const uint32_t* __restrict__ ubase, int64_t
                             v.y = bitf(a[it][1], il[it].y, g * CWB);
                             v.z = bitf(a[it][2], il[it].z, g * CWB);
                             v.w = bitf(a[it][3], il[it].w, g * CWB);
-                            reinterpret_cast<float4*>(o + g * K)[c] = v;
+                            st_out4(o + g * K + 4 * c, v);
                         }
                     }
                 }
@@ -802,7 +827,7 @@ __device__ __forceinline__ void emit(const uint32_t* __restrict__ ubase, int64_t
                             v.y = bitf(ub + (l4.y >> 5), l4.y, g * CWB);
                             v.z = bitf(ub + (l4.z >> 5), l4.z, g * CWB);
                             v.w = bitf(ub + (l4.w >> 5), l4.w, g * CWB);
-                            reinterpret_cast<float4*>(o + g * K)[c] = v;
+                            st_out4(o + g * K + 4 * c, v);
                         }
                     }
                 }
@@ -857,7 +882,7 @@ __device__ __forceinline__ void load_channel(float (&chv)[C::NS], const float* _
         // slots [0, NS/2) into VGPRs; slots [NS/2, NS) by LDS-DMA, one 256-byte LDS row per slot
         // (lane l's word at l * 4), so no VGPR holds them while the left half is decoded
 #pragma unroll
-        for (int j = 0; j < C::NS / 2; ++j) chv[j] = ch[j * C::G + res];
+        for (int j = 0; j < C::NS / 2; ++j) chv[j] = ld_ch(ch + j * C::G + res);
 #if PL_SC_DMA_ASM
         // saddr form: wave-uniform row base in an SGPR pair (slot offset j * 64 B as the 12-bit
         // immediate would also move the LDS address, so the base steps in SALU), this lane's
@@ -874,18 +899,22 @@ __device__ __forceinline__ void load_channel(float (&chv)[C::NS], const float* _
             const uint64_t sb = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a) |
                                 ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32);
             const uint32_t lb = (uint32_t)__builtin_amdgcn_readfirstlane((int)(lbase + (j - C::NS / 2) * 256));
+#if PL_SC_NT & 1
+            asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dword %0, %1 nt" ::"v"(voff), "s"(sb), "s"(lb) : "memory", "m0");
+#else
             asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dword %0, %1" ::"v"(voff), "s"(sb), "s"(lb) : "memory", "m0");
+#endif
         }
 #else
 #pragma unroll
         for (int j = C::NS / 2; j < C::NS; ++j)
             __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(ch + j * C::G + res),
                                              (__attribute__((address_space(3))) void*)(chl_wave + (j - C::NS / 2) * 64),
-                                             4, 0, 0);
+                                             4, 0, (PL_SC_NT & 1) ? 2 : 0);
 #endif
     } else {
 #pragma unroll
-        for (int j = 0; j < C::NS; ++j) chv[j] = ch[j * C::G + res];
+        for (int j = 0; j < C::NS; ++j) chv[j] = ld_ch(ch + j * C::G + res);
     }
 }
 

@@ -11,7 +11,7 @@
 constexpr int N = 1024, K = 512;
 constexpr long BS = 65536;
 
-template <int MODE, int MINW>
+template <int MODE, int MINW, int NT = 0>
 __global__ __launch_bounds__(256, MINW) void k(const float* __restrict__ llr, float* __restrict__ out) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const long cw0 = ((long)blockIdx.x * 4 + wave) * 4;
@@ -20,7 +20,7 @@ __global__ __launch_bounds__(256, MINW) void k(const float* __restrict__ llr, fl
         const float* ch = llr + (cw0 + (lane >> 4)) * N + (lane & 15);
         float v[64];
 #pragma unroll
-        for (int j = 0; j < 64; ++j) v[j] = ch[j * 16];
+        for (int j = 0; j < 64; ++j) v[j] = (NT & 2) ? __builtin_nontemporal_load(ch + j * 16) : ch[j * 16];
 #pragma unroll
         for (int j = 0; j < 64; ++j) acc += v[j];
     } else if constexpr (MODE == 1) {
@@ -48,37 +48,49 @@ __global__ __launch_bounds__(256, MINW) void k(const float* __restrict__ llr, fl
 #pragma unroll
     for (int g = 0; g < 4; ++g)
 #pragma unroll
-        for (int it = 0; it < 2; ++it) reinterpret_cast<float4*>(out + (cw0 + g) * K)[lane + 64 * it] = o;
+        for (int it = 0; it < 2; ++it) {
+            typedef float v4f __attribute__((ext_vector_type(4)));
+            v4f* p = reinterpret_cast<v4f*>(out + (cw0 + g) * K) + lane + 64 * it;
+            const v4f ov = {o.x, o.y, o.z, o.w};
+            if constexpr (NT & 1) __builtin_nontemporal_store(ov, p);
+            else *p = ov;
+        }
 }
 
 template <class F>
-float run(F kern, const float* in, float* out) {
+float run(F kern, float* const* in, float* const* out, int nbuf) {
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     const int blocks = BS / 16;
-    for (int r = 0; r < 20; ++r) kern<<<blocks, 256>>>(in, out);
+    for (int r = 0; r < 20; ++r) kern<<<blocks, 256>>>(in[r % nbuf], out[r % nbuf]);
     (void)hipEventRecord(e0);
-    for (int r = 0; r < 100; ++r) kern<<<blocks, 256>>>(in, out);
+    for (int r = 0; r < 96; ++r) kern<<<blocks, 256>>>(in[r % nbuf], out[r % nbuf]);
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
     float ms;
     (void)hipEventElapsedTime(&ms, e0, e1);
-    return ms / 100;
+    return ms / 96;
 }
 
 int main() {
-    float *in, *out;
-    (void)hipMalloc(&in, BS * N * 4);
-    (void)hipMalloc(&out, BS * K * 4);
-    (void)hipMemset(in, 0, BS * N * 4);
+    // 3 input and output buffers: rotating through them (1.15 GB) defeats the 256 MB Infinity
+    // Cache; the same buffer every launch lets the input stay partly resident there
+    float *in[3], *out[3];
+    for (int b = 0; b < 3; ++b) {
+        (void)hipMalloc(&in[b], BS * N * 4);
+        (void)hipMalloc(&out[b], BS * K * 4);
+        (void)hipMemset(in[b], 0, BS * N * 4);
+    }
     const double bytes = BS * (N + K) * 4.0;
     struct { const char* n; void (*k)(const float*, float*); } ks[] = {
         {"A residue dword (3 w/SIMD)", k<0, 3>}, {"A residue dword (2 w/SIMD)", k<0, 2>},
+        {"A + nt stores", k<0, 3, 1>}, {"A + nt loads", k<0, 3, 2>}, {"A + nt loads and stores", k<0, 3, 3>},
         {"B row-contig dword", k<1, 3>}, {"C dwordx4 4 rows", k<2, 3>}, {"D dwordx4 1 row", k<3, 3>}};
     for (auto& x : ks) {
-        float ms = run(x.k, in, out);
-        printf("%-30s %.4f ms  %.2f TB/s\n", x.n, ms, bytes / ms / 1e9);
+        const float same = run(x.k, in, out, 1), rot = run(x.k, in, out, 3);
+        printf("%-30s same buffers %.4f ms %.2f TB/s | rotating 3 buffers %.4f ms %.2f TB/s\n", x.n, same,
+               bytes / same / 1e9, rot, bytes / rot / 1e9);
     }
     return 0;
 }

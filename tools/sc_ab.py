@@ -83,7 +83,7 @@ def build(names, k, n, fm):
             print(*r, flush=True)
 
 
-def run(names, k, n, fm, rounds, bs, only=False):
+def run(names, k, n, fm, rounds, bs, only=False, rotate=1):
     import torch
 
     import polar_amd
@@ -120,14 +120,19 @@ def run(names, k, n, fm, rounds, bs, only=False):
             bad += int((got != want).any(dim=1).sum())
         print(f"{name}: {'exact' if bad == 0 else f'{bad} MISMATCHING ROWS'} vs the generic kernel", flush=True)
 
+    # rotate > 1: cycle through that many input/output buffer pairs, so the Infinity Cache
+    # (256 MB) cannot hold an input across launches
+    ins = [llr] + [llr.clone() for _ in range(rotate - 1)]
+    outs = [out] + [torch.empty_like(out) for _ in range(rotate - 1)]
+
     def tm(p, reps=20 if only else 200):
-        for _ in range(20):
-            ops.sc_decode(p, llr, out=out)
+        for r in range(20):
+            ops.sc_decode(p, ins[r % rotate], out=outs[r % rotate])
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        for _ in range(reps):
-            ops.sc_decode(p, llr, out=out)
+        for r in range(reps):
+            ops.sc_decode(p, ins[r % rotate], out=outs[r % rotate])
         e1.record()
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / reps
@@ -156,8 +161,9 @@ if __name__ == "__main__":
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--bs", type=int, default=65536)
     ap.add_argument("--only", action="store_true", help="run: time the named variants only (no base, no check)")
+    ap.add_argument("--rotate", type=int, default=1, help="run: cycle through this many input/output buffers")
     a = ap.parse_args()
     if a.cmd == "build":
         build(a.names, a.k, a.n, a.fm)
     else:
-        run(a.names, a.k, a.n, a.fm, a.rounds, a.bs, a.only)
+        run(a.names, a.k, a.n, a.fm, a.rounds, a.bs, a.only, a.rotate)
