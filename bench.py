@@ -97,7 +97,9 @@ def cpu_baseline(llr_host, fp, k, n, decoder, L, budget_s):
 def sim_iteration(plan, fp, k, n, bs, ebno, dev, reps=20):
     """One Monte-Carlo iteration of the harness on this GPU, measured
     after the timed region: the fused producer (pl_awgn_qpsk_llr: bits, encoder, QPSK, AWGN,
-    logits), the SC decode and the error counter (pl_count_errors), each by HIP events."""
+    logits), the SC decode and the error counter (pl_count_errors), each by HIP events; and the
+    path sim_ber takes for FusedAWGN + SC_Dec (pl_awgn_qpsk_llr_bits, packed bits, then
+    pl_sc_decode_count: decode and count in one kernel, no bit rows), timed as whole iterations."""
     from polar_amd import _lib, channel, ops
     enc = _lib.Plan(n, plan_mask(fp, n), 1, flags=_lib.PL_PLAN_GENERIC, device=dev)
     no = float(channel.ebnodb2no(ebno, 2, k / n))
@@ -118,8 +120,26 @@ def sim_iteration(plan, fp, k, n, bs, ebno, dev, reps=20):
         torch.cuda.synchronize(dev)
         t[name] = round(e0.elapsed_time(e1) / reps, 5)
     tot = sum(t.values())
-    return {"mcw_s": round(bs / tot / 1e3, 2), **t,
-            "note": "fused producer + SC decode + error count per iteration, one GPU, HIP events"}
+    res = {"mcw_s": round(bs / tot / 1e3, 2), **t,
+           "note": "fused producer + SC decode + error count per iteration, one GPU, HIP events"}
+    if plan.kernel()[0] == "specialized":
+        it = [2]
+
+        def fused_iter():
+            ub, lf = ops.awgn_qpsk_llr_bits(enc, bs, no, 42, it[0])
+            it[0] += 1
+            ops.sc_decode_count(plan, lf, ub, counts)
+        fused_iter()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            fused_iter()
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1) / reps
+        res["decode_count_path"] = {"mcw_s": round(bs / ms / 1e3, 2), "iteration_ms": round(ms, 5),
+                                    "note": "pl_awgn_qpsk_llr_bits + pl_sc_decode_count (sim_ber's path)"}
+    return res
 
 
 def plan_mask(fp, n):

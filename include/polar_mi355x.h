@@ -154,10 +154,24 @@ int pl_rate_recover(const float* llr, int64_t bs, int32_t e, const int32_t* src_
  *                  u_out (nullable): [bs, k] fp32 0/1; llr_out: [bs, n] fp32.  no > 0.
  * pl_count_errors: count_errors + count_block_errors (my_sn/sim.py:7-18) of two [rows, k] fp32 0/1
  *                  tensors: counts[0] += differing elements, counts[1] += rows with a difference
- *                  (int64 device counters, accumulated). */
+ *                  (int64 device counters, accumulated).
+ * pl_awgn_qpsk_llr_bits: pl_awgn_qpsk_llr with the information bits packed instead of fp32:
+ *                  ubits_out (nullable) [bs, ceil(k/32)] uint32, bit m % 32 of word m / 32 = bit m
+ *                  (bits past k zero).  Same stream, same logits.
+ * pl_sc_decode_count: SC decode (as pl_sc_decode) fused with the harness's error count: instead of
+ *                  writing the decided bits, compares them with ref_bits (packed as above) and
+ *                  accumulates counts[0] += bit errors, counts[1] += block errors (int64 device
+ *                  counters) -- pl_sc_decode + pl_count_errors in one pass (sim.py:84-100).
+ *                  workspace: pl_sc_count_workspace_size(plan, bs) bytes of device scratch.
+ *                  PL_ENOTSUP for plans on the generic SC kernel (pl_plan_kernel: 0). */
 int pl_awgn_qpsk_llr(const pl_plan* plan, uint64_t seed, uint64_t iteration, int64_t row0, int64_t bs, float no,
                      float* u_out, float* llr_out, void* hip_stream);
+int pl_awgn_qpsk_llr_bits(const pl_plan* plan, uint64_t seed, uint64_t iteration, int64_t row0, int64_t bs,
+                          float no, uint32_t* ubits_out, float* llr_out, void* hip_stream);
 int pl_count_errors(const float* a, const float* b, int64_t rows, int32_t k, int64_t* counts, void* hip_stream);
+size_t pl_sc_count_workspace_size(const pl_plan* plan, int64_t bs);
+int pl_sc_decode_count(const pl_plan* plan, const float* llr_logits, int64_t bs, const uint32_t* ref_bits,
+                       int64_t* counts, void* workspace, size_t ws_bytes, void* hip_stream);
 
 const char* pl_last_error_string(void);
 const char* pl_version(void);

@@ -242,6 +242,29 @@ class FusedAWGN(nn.Module):
             return None, bits_hat
         return bits, bits_hat
 
+    def error_counts(self, batch_size, ebno_db, counts=None):
+        """One Monte-Carlo iteration straight to the harness's counters: [bit errors, block errors]
+        (int64 [2] on the device, accumulated into counts) of decoding this iteration's batch --
+        what count_errors / count_block_errors (my_sn/sim.py:7-18) give on forward()'s output, for
+        the same draw.  The producer writes the information bits packed (pl_awgn_qpsk_llr_bits) and
+        the specialised SC kernel compares its decisions with them instead of writing bit rows
+        (pl_sc_decode_count).  Returns None (nothing drawn) when the decoder is not this package's
+        SC_Dec on a specialised plan; sim_ber then runs forward() and counts separately."""
+        from . import ops
+        from .decoders import SC_Dec
+        dec = self.decoder
+        if self.cw_estimates or type(dec) is not SC_Dec or dec.mode not in ("llr", "max"):
+            return None
+        plan = dec.plan(self.device)
+        if plan.kernel()[0] != "specialized":
+            return None
+        no = float(ebnodb2no(float(ebno_db), self.n_bits_per_sym, self.coderate))
+        it = self.iteration
+        self.iteration += 1
+        ubits, llr = ops.awgn_qpsk_llr_bits(self._plans.get(self.device, self._make_plan), int(batch_size), no,
+                                            self.seed, it, self.row0)
+        return ops.sc_decode_count(plan, llr, ubits, counts)
+
 
 def philox4x32_10(ctr, key):
     """Random123 Philox4x32-10 on numpy uint32 arrays: ctr [..., 4], key [..., 2] -> [..., 4].

@@ -242,6 +242,38 @@ int pl_sc_decode(const pl_plan* p, const float* llr, int64_t bs, void* out, int3
     return pl::launch_sc(p, llr, bs, out, out_kind, static_cast<hipStream_t>(stream));
 }
 
+size_t pl_sc_count_workspace_size(const pl_plan* p, int64_t bs) {
+    if (!p || bs <= 0 || !p->sc_module) return 0;
+    return (size_t)pl::sc_count_waves(p, bs) * 2 * sizeof(int32_t);
+}
+
+int pl_sc_decode_count(const pl_plan* p, const float* llr, int64_t bs, const uint32_t* ref_bits, int64_t* counts,
+                       void* ws, size_t ws_bytes, void* stream) {
+    if (!p || bs < 0 || !counts || (bs > 0 && p->k > 0 && (!llr || !ref_bits))) {
+        pl::set_error("pl_sc_decode_count: bad arguments");
+        return PL_EINVAL;
+    }
+    if (p->list_size != 1) {
+        pl::set_error("pl_sc_decode_count: needs an SC plan (list_size 1)");
+        return PL_EINVAL;
+    }
+    if (!p->sc_module || !p->sc_fn_cnt) {
+        pl::set_error("pl_sc_decode_count: the plan runs the generic SC kernel (no fused count); "
+                      "decode with pl_sc_decode and count with pl_count_errors");
+        return PL_ENOTSUP;
+    }
+    if (int r = pl::check_device(p, static_cast<hipStream_t>(stream), "pl_sc_decode_count")) return r;
+    if (bs == 0 || p->k == 0) return PL_OK;
+    if (ws_bytes < pl_sc_count_workspace_size(p, bs) || !ws) {
+        pl::set_error("pl_sc_decode_count: workspace too small (pl_sc_count_workspace_size)");
+        return PL_EINVAL;
+    }
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    int32_t* part = static_cast<int32_t*>(ws);
+    if (int r = pl::launch_sc_static_count(p, llr, bs, ref_bits, part, st)) return r;
+    return pl::launch_sum_pairs(part, pl::sc_count_waves(p, bs), counts, st);
+}
+
 size_t pl_scl_workspace_size(const pl_plan* p, int64_t bs) { return p ? pl::scl_workspace_size(p, bs) : 0; }
 
 int pl_scl_decode(const pl_plan* p, const float* llr, int64_t bs, void* out, int32_t out_kind, double* out_pm,

@@ -24,6 +24,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 #include "../../../include/polar_mi355x.h"
 #include "plan.h"
 
@@ -76,7 +78,8 @@ constexpr int kWordsPerWave = 256;  // LDS words per wave: stream words (<= 128)
 
 __global__ __launch_bounds__(256) void awgn_llr_kernel(int64_t bs, int64_t row0, uint32_t k0, uint32_t k1, uint32_t it,
                                                        float no, const uint32_t* __restrict__ frozen_words, int n, int k,
-                                                       float* __restrict__ u_out, float* __restrict__ llr_out) {
+                                                       float* __restrict__ u_out, float* __restrict__ llr_out,
+                                                       uint32_t* __restrict__ ubits_out) {
     __shared__ uint32_t lds[4 * kWordsPerWave];
     const int wpc = n >= 32 ? n / 32 : 1, cpw = 64 / wpc, nb = n >= 32 ? 32 : n;
     const int nq = (k + 31) / 32;  // stream words per row
@@ -150,24 +153,37 @@ __global__ __launch_bounds__(256) void awgn_llr_kernel(int64_t bs, int64_t row0,
             }
         }
     }
+    // C1': the information bits packed, ceil(k/32) words per row (bit m of a row = bit m % 32 of
+    // word m / 32: the stream words themselves, bits past k cleared) -- the decode+count kernel's
+    // reference (pl_sc_decode_count), 1/32 of the fp32 rows' bytes
+    if (ubits_out != nullptr && k > 0) {
+        const uint32_t last = (k & 31) ? ((1u << (k & 31)) - 1u) : 0xFFFFFFFFu;
+        for (int r = 0; r < rows; ++r)
+            for (int q = lane; q < nq; q += 64) ubits_out[(b0 + r) * nq + q] = sw[r * nq + q] & (q == nq - 1 ? last : 0xFFFFFFFFu);
+    }
     // C2: logits.  QPSK component of code bit j: (1 - 2 c_j)/sqrt(2) plus sqrt(no) * N(0, 1/2)
     // (awgn.py:24-29, utils.py:11-15); logit = -2 sqrt(2) y / no.  Chunk c of a row = positions
     // [CH c, CH c + CH) draws noise block c (4 uniforms -> 2 Box-Muller pairs).
     const float sn = sqrtf(no) * 0.70710677f, a = 0.70710677f, scale = -2.8284271f / no;
-    const int CH = n >= 4 ? 4 : n, nch = n / CH;
+    const int CH = n >= 4 ? 4 : n, nch = n / CH, lnch = __builtin_ctz(nch);  // n is a power of two
     const bool vec = CH == 4 && ((reinterpret_cast<uintptr_t>(llr_out) & 15) == 0);
     for (int c = lane; c < rows * nch; c += 64) {
-        const int r = c / nch, ch = c - r * nch, p = ch * CH;
+        const int r = c >> lnch, ch = c & (nch - 1), p = ch * CH;
         const U4 rnd = stream_block(k0, k1, row0 + b0 + r, it, 1, (uint32_t)ch);
-        const float r0 = sqrtf(-2.0f * __logf(unit(rnd.x))), r1 = sqrtf(-2.0f * __logf(unit(rnd.z)));
-        float s0, c0, s1, c1;
-        __sincosf(6.2831853f * unit(rnd.y), &s0, &c0);
-        __sincosf(6.2831853f * unit(rnd.w), &s1, &c1);
-        const float z[4] = {r0 * c0, r0 * s0, r1 * c1, r1 * s1};
+        // Box-Muller on the hardware transcendentals: the uniforms lie in [2^-25, 1), so v_log_f32
+        // (log2) needs no denormal scaling; v_sin/v_cos take revolutions, sin(2 pi u) = v_sin(u).
+        // (A noise draw, not a decoder value: only its distribution is specified.)
+        const float ln2 = 0.69314718f;
+        const float r0 = __builtin_amdgcn_sqrtf(-2.0f * ln2 * __builtin_amdgcn_logf(unit(rnd.x)));
+        const float r1 = __builtin_amdgcn_sqrtf(-2.0f * ln2 * __builtin_amdgcn_logf(unit(rnd.z)));
+        const float ty = unit(rnd.y), tw = unit(rnd.w);
+        const float z[4] = {r0 * __builtin_amdgcn_cosf(ty), r0 * __builtin_amdgcn_sinf(ty),
+                            r1 * __builtin_amdgcn_cosf(tw), r1 * __builtin_amdgcn_sinf(tw)};
         const uint32_t bits = cwd[r * wpc + (p >> 5)] >> (p & 31);
         float l[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) l[i] = scale * ((((bits >> i) & 1u) ? -a : a) + sn * z[i]);
+        for (int i = 0; i < 4; ++i)  // (1 - 2 c) a: the code bit moved to the sign of a
+            l[i] = scale * (__uint_as_float(__float_as_uint(a) ^ ((bits << (31 - i)) & 0x80000000u)) + sn * z[i]);
         float* o = llr_out + (b0 + r) * n + p;
         if (vec) {
             *reinterpret_cast<float4*>(o) = float4{l[0], l[1], l[2], l[3]};
@@ -231,29 +247,81 @@ __global__ __launch_bounds__(256) void count_errors_kernel(const float* __restri
     }
 }
 
+// counts[0..1] += sums of the [bit, block] error pairs the decode+count kernel stored per wave:
+// kSumBlocks blocks, one pair of atomics each (no contention worth the name on the two counters)
+constexpr int kSumBlocks = 64;
+
+__global__ __launch_bounds__(256) void sum_pairs_kernel(const int32_t* __restrict__ part, int64_t pairs,
+                                                        unsigned long long* __restrict__ counts) {
+    __shared__ unsigned long long red[4][2];
+    unsigned long long be = 0, ke = 0;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < pairs; i += (int64_t)gridDim.x * 256) {
+        be += (uint32_t)part[2 * i];
+        ke += (uint32_t)part[2 * i + 1];
+    }
+    for (int off = 32; off >= 1; off >>= 1) {
+        be += __shfl_xor(be, off, 64);
+        ke += __shfl_xor(ke, off, 64);
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane == 0) {
+        red[wv][0] = be;
+        red[wv][1] = ke;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long b = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+        const unsigned long long e = red[0][1] + red[1][1] + red[2][1] + red[3][1];
+        if (b) atomicAdd(&counts[0], b);
+        if (e) atomicAdd(&counts[1], e);
+    }
+}
+
 }  // namespace
+
+namespace pl {
+int launch_sum_pairs(const int32_t* part, int64_t pairs, int64_t* counts, hipStream_t stream) {
+    if (pairs <= 0) return PL_OK;
+    const int64_t need = (pairs + 255) / 256;
+    const unsigned blocks = (unsigned)(need < kSumBlocks ? need : kSumBlocks);
+    hipLaunchKernelGGL(sum_pairs_kernel, dim3(blocks), dim3(256), 0, stream, part, pairs,
+                       reinterpret_cast<unsigned long long*>(counts));
+    return check_hip(hipGetLastError(), "sum_pairs launch");
+}
+}  // namespace pl
 
 extern "C" {
 
-int pl_awgn_qpsk_llr(const pl_plan* p, uint64_t seed, uint64_t iteration, int64_t row0, int64_t bs, float no,
-                     float* u_out, float* llr_out, void* stream) {
+static int awgn_launch(const pl_plan* p, uint64_t seed, uint64_t iteration, int64_t row0, int64_t bs, float no,
+                       float* u_out, uint32_t* ubits_out, float* llr_out, void* stream, const char* what) {
     if (!p || bs < 0 || row0 < 0 || (bs > 0 && !llr_out) || !(no > 0.0f)) {
-        pl::set_error("pl_awgn_qpsk_llr: bad arguments (no must be > 0)");
+        pl::set_error(std::string(what) + ": bad arguments (no must be > 0)");
         return PL_EINVAL;
     }
-    if (int r = pl::check_device(p, static_cast<hipStream_t>(stream), "pl_awgn_qpsk_llr")) return r;
+    if (int r = pl::check_device(p, static_cast<hipStream_t>(stream), what)) return r;
     if (bs == 0) return PL_OK;
     const int wpc = p->n >= 32 ? p->n / 32 : 1;
     const int64_t cpw = 64 / wpc;
     const int64_t blocks = ((bs + cpw - 1) / cpw + 3) / 4;
     if (blocks > 0x7fffffffLL) {
-        pl::set_error("pl_awgn_qpsk_llr: batch too large for one launch");
+        pl::set_error(std::string(what) + ": batch too large for one launch");
         return PL_EINVAL;
     }
     hipLaunchKernelGGL(awgn_llr_kernel, dim3((unsigned)blocks), dim3(256), 0, static_cast<hipStream_t>(stream), bs,
                        row0, (uint32_t)seed, (uint32_t)(seed >> 32), (uint32_t)iteration, no, p->d_frozen_words, p->n,
-                       p->k, u_out, llr_out);
-    return pl::check_hip(hipGetLastError(), "pl_awgn_qpsk_llr launch");
+                       p->k, u_out, llr_out, ubits_out);
+    return pl::check_hip(hipGetLastError(), what);
+}
+
+int pl_awgn_qpsk_llr(const pl_plan* p, uint64_t seed, uint64_t iteration, int64_t row0, int64_t bs, float no,
+                     float* u_out, float* llr_out, void* stream) {
+    return awgn_launch(p, seed, iteration, row0, bs, no, u_out, nullptr, llr_out, stream, "pl_awgn_qpsk_llr");
+}
+
+int pl_awgn_qpsk_llr_bits(const pl_plan* p, uint64_t seed, uint64_t iteration, int64_t row0, int64_t bs, float no,
+                          uint32_t* ubits_out, float* llr_out, void* stream) {
+    return awgn_launch(p, seed, iteration, row0, bs, no, nullptr, ubits_out, llr_out, stream,
+                       "pl_awgn_qpsk_llr_bits");
 }
 
 int pl_count_errors(const float* a, const float* b, int64_t rows, int32_t k, int64_t* counts, void* stream) {

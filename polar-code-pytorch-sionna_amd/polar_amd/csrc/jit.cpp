@@ -281,6 +281,11 @@ int attach_static(pl_plan* p, const uint8_t* frozen, bool allow_compile) {
     hipFunction_t f32, u8;
     r = check_hip(hipModuleGetFunction(&f32, mod, "pl_sc_static_f32"), "hipModuleGetFunction");
     if (!r) r = check_hip(hipModuleGetFunction(&u8, mod, "pl_sc_static_u8"), "hipModuleGetFunction");
+    hipFunction_t cnt = nullptr;  // optional (absent from diagnostic builds): decode + error count
+    if (!r && hipModuleGetFunction(&cnt, mod, "pl_sc_static_cnt") != hipSuccess) {
+        cnt = nullptr;
+        (void)hipGetLastError();
+    }
     // info_loc[m]: where the u bit of information position m sits in a wave's LDS u words
     // (sc_static.h emit): (byte offset of its word in codeword 0's area) << 5 | bit in the word
     const int lg = static_log_g(p->log_n, p->f_mode);
@@ -321,6 +326,7 @@ int attach_static(pl_plan* p, const uint8_t* frozen, bool allow_compile) {
     p->sc_module = mod;
     p->sc_fn_f32 = f32;
     p->sc_fn_u8 = u8;
+    p->sc_fn_cnt = cnt;
     p->kernel_path = path;
     return PL_OK;
 }
@@ -328,7 +334,32 @@ int attach_static(pl_plan* p, const uint8_t* frozen, bool allow_compile) {
 void detach_static(pl_plan* p) {
     if (p->sc_module) (void)hipModuleUnload(p->sc_module);
     p->sc_module = nullptr;
-    p->sc_fn_f32 = p->sc_fn_u8 = nullptr;
+    p->sc_fn_f32 = p->sc_fn_u8 = p->sc_fn_cnt = nullptr;
+}
+
+int64_t sc_count_waves(const pl_plan* p, int64_t bs) {
+    const int64_t per_block = 4 * (64 / (1 << p->sc_log_g));
+    return ((bs + per_block - 1) / per_block) * 4;
+}
+
+int launch_sc_static_count(const pl_plan* p, const float* llr, int64_t bs, const uint32_t* ref, int32_t* part,
+                           hipStream_t st) {
+    if (bs == 0 || p->k == 0) return PL_OK;
+    if (p->sc_persistent) {
+        set_error("SC decode+count: the plan's kernel is a persistent diagnostic build");
+        return PL_ENOTSUP;
+    }
+    const int64_t blocks = sc_count_waves(p, bs) / 4;
+    if (blocks > 0x7fffffffLL) {
+        set_error("SC decode+count: batch too large for one launch");
+        return PL_EINVAL;
+    }
+    const float lmax = p->llr_max;
+    int k = p->k;
+    const int32_t* loc = p->d_info_loc;
+    void* args[] = {(void*)&llr, (void*)&bs, (void*)&part, (void*)&loc, (void*)&k, (void*)&lmax, (void*)&ref};
+    return check_hip(hipModuleLaunchKernel(p->sc_fn_cnt, (unsigned)blocks, 1, 1, 256, 1, 1, 0, st, args, nullptr),
+                     "SC decode+count launch (specialised)");
 }
 
 int launch_sc_static(const pl_plan* p, const float* llr, int64_t bs, void* out, int out_kind, hipStream_t st) {

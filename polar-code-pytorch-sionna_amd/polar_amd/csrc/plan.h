@@ -21,6 +21,7 @@ struct pl_plan {
     int32_t* d_info_loc = nullptr;       // k (padded to 4): (lane-in-group << 8) | slot of info bit m
     hipModule_t sc_module = nullptr;
     hipFunction_t sc_fn_f32 = nullptr, sc_fn_u8 = nullptr;
+    hipFunction_t sc_fn_cnt = nullptr;   // decode + error count (pl_sc_decode_count); null if absent
     std::string kernel_path;             // code object the module came from
     int32_t crc_deg = 0;                 // SCL CRC-aided pick: degree (0 = none) and generator
     uint32_t crc_g = 0;                  //   mask without the leading term
@@ -54,4 +55,11 @@ int attach_static(pl_plan* plan, const uint8_t* frozen_mask, bool allow_compile)
 void detach_static(pl_plan* plan);
 int launch_sc_static(const pl_plan* plan, const float* llr, int64_t bs, void* out, int out_kind,
                      hipStream_t stream);
+// decode + count (specialised kernel's pl_sc_static_cnt): per-wave [bit, block] error pairs into
+// part (int32[2 * waves]), waves = sc_count_waves(plan, bs)
+int64_t sc_count_waves(const pl_plan* plan, int64_t bs);
+int launch_sc_static_count(const pl_plan* plan, const float* llr, int64_t bs, const uint32_t* ref, int32_t* part,
+                           hipStream_t stream);
+// counts[0..1] += the sums of the [bit, block] pairs of part (channel_kernel.hip)
+int launch_sum_pairs(const int32_t* part, int64_t pairs, int64_t* counts, hipStream_t stream);
 }  // namespace pl

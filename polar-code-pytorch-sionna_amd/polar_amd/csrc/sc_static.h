@@ -118,7 +118,7 @@ typedef unsigned long uintptr_t;
 namespace pls {
 
 enum : int { R0 = 0, R1 = 1, REP = 2, SPC = 3, GEN = 4 };
-enum : int { OUT_F32 = 0, OUT_U8 = 1 };
+enum : int { OUT_F32 = 0, OUT_U8 = 1, OUT_CNT = 2 };
 constexpr int kWaves = 4;  // waves per workgroup
 
 template <bool B, class T, class F>
@@ -852,6 +852,54 @@ __device__ __forceinline__ void emit(const uint32_t* __restrict__ ubase, int64_t
     }
 }
 
+// OUT_CNT (the Monte-Carlo harness fused into the decoder, my_sn/sim.py:7-18 count_errors /
+// count_block_errors): instead of writing the [bs, k] bit rows, compare the decoded information
+// bits with the reference bits (packed, bit m of row r = bit m % 32 of ref[r * NQ + m / 32]) and
+// store the wave's [bit errors, block errors] at part[2 * wave id] (int32; pl_sc_decode_count sums
+// them).  Every wave of the grid stores its pair, rows past bs count nothing.
+template <class C>
+__device__ __forceinline__ void count_emit(const uint32_t* __restrict__ ubase, int64_t cw0, int64_t bs,
+                                           const uint32_t* __restrict__ ref, int32_t* __restrict__ part,
+                                           const int32_t* __restrict__ info_loc, int lane, int wid) {
+    // Lane l takes information bits m = l + 64 it; a ballot over the wave packs bits 64 it .. 64 it
+    // + 63 of a codeword into the same two words the reference row holds there, so the comparison
+    // is a scalar XOR + popcount against a wave-uniform (scalar) load of those words.
+    using E = Emit<C>;
+    constexpr int K = C::K, CW = E::CW, CWB = E::CWB, NQ = (K + 31) / 32;
+    const unsigned char* ub = reinterpret_cast<const unsigned char*>(ubase);
+    uint32_t bits = 0, blocks = 0;
+    int loc[E::IT1];
+#pragma unroll
+    for (int it = 0; it < E::IT1; ++it) {
+        const int m = lane + 64 * it;
+        loc[it] = (K % 64 == 0 || m < K) ? info_loc[m] : -1;
+    }
+#pragma unroll
+    for (int g = 0; g < CW; ++g) {
+        if (cw0 + g >= bs) break;  // wave-uniform
+        const uint32_t* rrow = ref + (cw0 + g) * NQ;
+        uint64_t diff = 0;
+#pragma unroll
+        for (int it = 0; it < E::IT1; ++it) {
+            uint32_t b = 0;
+            if (loc[it] >= 0) {
+                const uint32_t w = *reinterpret_cast<const uint32_t*>(ub + (loc[it] >> 5) + g * CWB);
+                b = __builtin_amdgcn_ubfe(w, (uint32_t)loc[it], 1u);
+            }
+            const uint64_t dec = __builtin_amdgcn_ballot_w64(b != 0u);
+            const uint64_t want = (uint64_t)rrow[2 * it] | (2 * it + 1 < NQ ? (uint64_t)rrow[2 * it + 1] << 32 : 0ull);
+            const uint64_t x = dec ^ want;
+            bits += (uint32_t)__builtin_popcountll(x);
+            diff |= x;
+        }
+        blocks += diff != 0 ? 1u : 0u;
+    }
+    if (lane == 0) {
+        part[2 * wid] = (int32_t)bits;
+        part[2 * wid + 1] = (int32_t)blocks;
+    }
+}
+
 // this lane's float4-path table entries, loaded early (their latency hides behind the channel)
 template <class C>
 __device__ __forceinline__ void preload_info(const int32_t* __restrict__ info_loc, int4 (&il)[2], int lane) {
@@ -954,7 +1002,8 @@ __device__ __forceinline__ void root_virtual(float (&chv)[C::NS], const Lane& ln
 template <class C, int OUT>
 __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs, void* __restrict__ out,
                                        const int32_t* __restrict__ info_loc, int k, float lmax,
-                                       uint32_t* __restrict__ ulds) {
+                                       uint32_t* __restrict__ ulds, const uint32_t* __restrict__ ref = nullptr) {
+    static_assert(OUT != OUT_CNT || (!PL_SC_PERSIST && !PL_SC_STAMPS), "OUT_CNT: plain decoder only");
     constexpr int N = C::N, G = C::G, LG = C::LOG_G, NS = C::NS, CW = 64 / G;
     constexpr int WPL = (NS + 31) / 32;
     // the wave index is wave-uniform: as an SGPR value all batch/row address math is scalar
@@ -1088,7 +1137,10 @@ __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs
 #if PL_SC_STAMPS
     uint64_t st3 = __builtin_amdgcn_s_memtime();
 #endif
-    emit<C, OUT>(ubase, cw0, bs, out, info_loc, il, lane);
+    if constexpr (OUT == OUT_CNT)
+        count_emit<C>(ubase, cw0, bs, ref, static_cast<int32_t*>(out), info_loc, lane, blockIdx.x * kWaves + wave);
+    else
+        emit<C, OUT>(ubase, cw0, bs, out, info_loc, il, lane);
 #if PL_SC_STAMPS
     __builtin_amdgcn_s_waitcnt(0);
     uint64_t st4 = __builtin_amdgcn_s_memtime();
@@ -1236,10 +1288,24 @@ __device__ __forceinline__ void decode_staged(const float* __restrict__ llr, int
 #ifndef PL_SC_PERSIST_BPC
 #define PL_SC_PERSIST_BPC 2  // resident blocks per CU the launcher gives a persistent kernel
 #endif
+// decode + error count against packed reference bits (pl_sc_decode_count); plain decoder only
+#if PL_SC_PERSIST || PL_SC_STAMPS || PL_SC_ROOT_MODE
+#define PL_SC_CNT_ENTRY(CODE)
+#else
+#define PL_SC_CNT_ENTRY(CODE)                                                                                \
+    extern "C" __global__ __launch_bounds__(64 * pls::kWaves, PL_SC_MINW) void pl_sc_static_cnt(             \
+        const float* __restrict__ llr, int64_t bs, int32_t* __restrict__ part, const int32_t* __restrict__ info_loc, \
+        int k, float lmax, const uint32_t* __restrict__ ref) {                                               \
+        __shared__ uint32_t ulds[pls::Ch<CODE>::CHL ? pls::kWaves * 64 * (CODE::NS / 2)                       \
+                                                    : pls::kWaves * 64 * ((CODE::NS + 31) / 32)];              \
+        pls::decode<CODE, pls::OUT_CNT>(llr, bs, part, info_loc, k, lmax, ulds, ref);                        \
+    }
+#endif
 #define PL_SC_STATIC_KERNELS(CODE)                                                                           \
     extern "C" __device__ const int pl_sc_persistent = PL_SC_PERSIST;                                       \
     extern "C" __device__ const int pl_sc_blocks_per_cu = PL_SC_PERSIST_BPC;                                \
     PL_SC_ENTRY(CODE, pl_sc_static_f32, pls::OUT_F32)                                                        \
-    PL_SC_ENTRY(CODE, pl_sc_static_u8, pls::OUT_U8)
+    PL_SC_ENTRY(CODE, pl_sc_static_u8, pls::OUT_U8)                                                          \
+    PL_SC_CNT_ENTRY(CODE)
 
 #endif  // PL_SC_STATIC_H

@@ -115,6 +115,64 @@ def awgn_qpsk_llr(plan, bs, no, seed, iteration, row0=0, with_bits=True):
     return u, llr
 
 
+def awgn_qpsk_llr_bits(plan, bs, no, seed, iteration, row0=0):
+    """pl_awgn_qpsk_llr_bits: the fused producer with the information bits packed -- returns
+    (ubits [bs, ceil(k/32)] int32 words, bit m % 32 of word m // 32 = bit m; logits [bs, n] fp32).
+    Same stream and logits as awgn_qpsk_llr."""
+    dev = plan.device
+    no = float(no)
+    if not no > 0.0:
+        raise ValueError(f"noise variance must be positive, got {no}")
+    llr = torch.empty((bs, plan.n), dtype=torch.float32, device=dev)
+    ubits = torch.empty((bs, (plan.k + 31) // 32), dtype=torch.int32, device=dev)
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().pl_awgn_qpsk_llr_bits(plan.handle, int(seed) & (2 ** 64 - 1),
+                                                    int(iteration) & (2 ** 64 - 1), int(row0), int(bs), no,
+                                                    ctypes.c_void_p(ubits.data_ptr()), ctypes.c_void_p(llr.data_ptr()),
+                                                    _lib.current_stream_ptr(dev)),
+                   "pl_awgn_qpsk_llr_bits")
+    return ubits, llr
+
+
+def pack_bits(bits):
+    """[..., k] 0/1 tensor -> [rows, ceil(k/32)] int32 words in pl_sc_decode_count's layout."""
+    k = bits.shape[-1]
+    b = (bits.reshape(-1, k) != 0).to(torch.int64)
+    nq = (k + 31) // 32
+    b = torch.nn.functional.pad(b, (0, nq * 32 - k)).reshape(-1, nq, 32)
+    w = (b << torch.arange(32, device=b.device, dtype=torch.int64)).sum(-1)
+    return torch.where(w >= 2 ** 31, w - 2 ** 32, w).to(torch.int32)
+
+
+
+def sc_decode_count(plan, llr_logits, ref_bits, counts=None):
+    """pl_sc_decode_count: SC decode fused with count_errors / count_block_errors (my_sn/sim.py:7-18)
+    against packed reference bits (awgn_qpsk_llr_bits / pack_bits); accumulates [bit errors, block
+    errors] into counts (int64 [2] on the device, created if None) and returns it.  Raises
+    PolarLibError (PL_ENOTSUP) for a plan on the generic SC kernel."""
+    _require_cuda(llr_logits, "llr_logits")
+    x = llr_logits
+    if x.dtype != torch.float32 or not x.is_contiguous():
+        x = x.to(torch.float32).contiguous()
+    if x.dim() != 2 or x.shape[1] != plan.n:
+        raise ValueError(f"llr_logits must be [bs, {plan.n}], got {tuple(x.shape)}")
+    bs = x.shape[0]
+    nq = (plan.k + 31) // 32
+    if ref_bits.shape != (bs, nq) or ref_bits.dtype != torch.int32 or ref_bits.device != x.device:
+        raise ValueError(f"ref_bits must be int32 [{bs}, {nq}] on the input's device")
+    ref = ref_bits.contiguous()
+    if counts is None:
+        counts = torch.zeros(2, dtype=torch.int64, device=x.device)
+    ws_bytes = int(_lib.lib().pl_sc_count_workspace_size(plan.handle, bs))
+    ws = torch.empty((max(ws_bytes, 4),), dtype=torch.uint8, device=x.device)  # per call: stream-safe
+    with torch.cuda.device(x.device):
+        _lib.check(_lib.lib().pl_sc_decode_count(plan.handle, ctypes.c_void_p(x.data_ptr()), bs,
+                                                 ctypes.c_void_p(ref.data_ptr()), ctypes.c_void_p(counts.data_ptr()),
+                                                 ctypes.c_void_p(ws.data_ptr()), ws_bytes,
+                                                 _lib.current_stream_ptr(x.device)), "pl_sc_decode_count")
+    return counts
+
+
 def count_errors(a, b, counts=None):
     """[bit errors, block errors] (int64, on the device) of two [..., k] 0/1 fp32 tensors
     (my_sn/sim.py:7-18 count_errors / count_block_errors in one pass); accumulates into counts."""

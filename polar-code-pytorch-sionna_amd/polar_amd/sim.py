@@ -53,22 +53,22 @@ def sim_ber(mc_fun, ebno_dbs, batch_size, max_mc_iter, soft_estimates=False, tar
     cnt = tc.zeros([P, 4], dtype=tc.int64, device=cdev)
     status = tc.zeros(P)
     runtime = np.zeros(P)
+    # channel.FusedAWGN with this package's SC decoder: decode and count in one kernel, no bit rows
+    fused = None if soft_estimates else getattr(getattr(mc_fun, "__self__", mc_fun), "error_counts", None)
     for i in range(P):
         t0 = time.perf_counter()
         it = -1
         for ii in range(max_mc_iter):
             it += 1
-            b, b_hat = mc_fun(batch_size=batch_size, ebno_db=ebno_dbs[i])
-            if soft_estimates:
-                b_hat = hard_decisions(b_hat)
-            if b.is_cuda and b_hat.is_cuda and b.shape == b_hat.shape and b.shape[-1] > 0:
-                # both counters in one HIP pass (pl_count_errors), no torch reductions
-                from . import ops
-                be = ops.count_errors(b, b_hat)
-                inc = tc.cat([be, tc.tensor([b.numel(), b.numel() // b.shape[-1]], dtype=tc.int64, device=b.device)])
+            be = fused(batch_size, ebno_dbs[i]) if fused is not None else None
+            if be is not None:
+                k = getattr(mc_fun, "__self__", mc_fun).k
+                inc = tc.cat([be, tc.tensor([batch_size * k, batch_size], dtype=tc.int64, device=be.device)])
             else:
-                inc = tc.stack([count_errors(b, b_hat), count_block_errors(b, b_hat),
-                                tc.tensor(b.numel(), device=b.device), tc.tensor(b.numel() // b.shape[-1], device=b.device)])
+                b, b_hat = mc_fun(batch_size=batch_size, ebno_db=ebno_dbs[i])
+                if soft_estimates:
+                    b_hat = hard_decisions(b_hat)
+                inc = _increment(b, b_hat)
             inc = inc.to(cdev)
             if dist is not None:
                 dist.all_reduce(inc, op=dist.ReduceOp.SUM, group=process_group)
@@ -104,6 +104,17 @@ def sim_ber(mc_fun, ebno_dbs, batch_size, max_mc_iter, soft_estimates=False, tar
     if return_counts:
         return ber, bler, c
     return ber, bler
+
+
+def _increment(b, b_hat):
+    """[bit errors, block errors, bits, blocks] of one iteration (sim.py:84-100)."""
+    if b.is_cuda and b_hat.is_cuda and b.shape == b_hat.shape and b.shape[-1] > 0:
+        # both counters in one HIP pass (pl_count_errors), no torch reductions
+        from . import ops
+        be = ops.count_errors(b, b_hat)
+        return tc.cat([be, tc.tensor([b.numel(), b.numel() // b.shape[-1]], dtype=tc.int64, device=b.device)])
+    return tc.stack([count_errors(b, b_hat), count_block_errors(b, b_hat),
+                     tc.tensor(b.numel(), device=b.device), tc.tensor(b.numel() // b.shape[-1], device=b.device)])
 
 
 def _cells(ebno, host, rt, status_txt):

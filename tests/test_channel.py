@@ -39,3 +39,16 @@ def test_fused_info_bits_layout():
     w = philox4x32_10(np.array([12, 0, 3, 0], dtype=np.uint64), np.array([42, 0], dtype=np.uint64))
     assert [int(b) for b in u[2, 32:64]] == [(int(w[1]) >> i) & 1 for i in range(32)]
     assert abs(fused_info_bits(1, 0, np.arange(2000), 512).mean() - 0.5) < 0.01
+
+
+def test_pack_bits_layout():
+    """ops.pack_bits: bit m of a row = bit m % 32 of word m // 32 (pl_sc_decode_count's reference)."""
+    import torch
+    from polar_amd import ops
+    rng = np.random.default_rng(4)
+    for k in (1, 31, 32, 33, 48, 512):
+        b = rng.integers(0, 2, (7, k))
+        w = ops.pack_bits(torch.from_numpy(b).float()).numpy().view(np.uint32)
+        assert w.shape == (7, (k + 31) // 32)
+        for m in range(k):
+            assert np.array_equal((w[:, m // 32] >> np.uint32(m % 32)) & 1, b[:, m])

@@ -49,3 +49,8 @@ t_all, _ = timed(lambda: model(a.bs, eb))
 print(f"({a.k},{a.n}) bs={a.bs} producer={a.producer}: LLR production {t_llr:.3f} ms, decode {t_dec:.3f} ms, "
       f"counting {t_cnt:.3f} ms, model() {t_all:.3f} ms -> {a.bs / t_all / 1e3:.1f} Mcw/s end to end, "
       f"BLER {float(sim.count_block_errors(bits, bh)) / a.bs:.4f}", flush=True)
+if a.producer == "fused":
+    counts = torch.zeros(2, dtype=torch.int64, device=dev)
+    t_fc, _ = timed(lambda: model.error_counts(a.bs, eb, counts), reps=50)
+    print(f"  sim_ber's fused path (pl_awgn_qpsk_llr_bits + pl_sc_decode_count): {t_fc:.3f} ms per iteration -> "
+          f"{a.bs / t_fc / 1e3:.1f} Mcw/s", flush=True)
