@@ -868,7 +868,7 @@ __device__ __forceinline__ void count_emit(const uint32_t* __restrict__ ubase, i
     constexpr int K = C::K, CW = E::CW, CWB = E::CWB, NQ = (K + 31) / 32;
     const unsigned char* ub = reinterpret_cast<const unsigned char*>(ubase);
     uint32_t bits = 0, blocks = 0;
-    int loc[E::IT1];
+    int loc[E::IT1 > 0 ? E::IT1 : 1];
 #pragma unroll
     for (int it = 0; it < E::IT1; ++it) {
         const int m = lane + 64 * it;

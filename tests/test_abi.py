@@ -6,6 +6,7 @@ import ctypes
 import os
 import re
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -170,3 +171,42 @@ def test_generated_source_names_compiler_and_flags():
     assert "--genco" in flags and "--offload-arch=gfx950" in flags
     assert compiler and compiler in _lib.hipcc_version(_lib.hipcc_path())
     assert name.startswith("sc_") and name.endswith(".co")
+
+
+def test_specialised_source_compiles_for_edge_codes():
+    """The specialised SC kernel source (every entry: f32, u8 and decode+count) compiles for the
+    edge codes a plan may be asked for -- k = 0, k = 1, k = n - 1, k = n -- at several n, both f
+    modes (hipcc -fsyntax-only; the GPU tests only compile the codes they decode)."""
+    import shutil
+    import subprocess
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
+    from polar_amd import _lib
+    hipcc = _lib.hipcc_path()
+    if hipcc is None or shutil.which(hipcc) is None and not os.path.exists(hipcc):
+        pytest.skip("hipcc not available")
+    jobs = []
+    for n in (2, 64, 1024, 2048):
+        for kind in ("k0", "k1", "kn-1", "kn"):
+            m = np.zeros(n, np.uint8)
+            if kind == "k0":
+                m[:] = 1
+            elif kind == "k1":
+                m[:-1] = 1
+            elif kind == "kn-1":
+                m[0] = 1
+            for fm in (0, 1):
+                jobs.append((n, kind, fm, m))
+    tmp = tempfile.mkdtemp()
+
+    def one(job):
+        n, kind, fm, m = job
+        src, _ = _lib.sc_source(n, m, fm)
+        f = os.path.join(tmp, f"c_{n}_{kind}_{fm}.hip")
+        open(f, "w").write(src)
+        r = subprocess.run([hipcc, "--offload-arch=gfx950", "--cuda-device-only", "-fsyntax-only", "-std=c++17", f],
+                           capture_output=True, text=True)
+        return job[:3], r.returncode, r.stderr[-600:]
+    with ThreadPoolExecutor(8) as ex:
+        bad = [(j, e) for j, rc, e in ex.map(one, jobs) if rc]
+    assert not bad, bad[:2]
