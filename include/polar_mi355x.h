@@ -26,6 +26,7 @@
  *   pl_polar_encode  PolarEncoder.forward x_run_sn_polar/polar/enc.py:30-43
  *                    (butterfly form of my_sn/fec/polar/enc.py:85-96)
  *   pl_crc_attach    CRCEncoder.forward my_sn/fec/crc.py:85-104 (G-matrix CRC, 5G polynomials :38-52)
+ *   pl_crc_check     CRCDecoder.forward my_sn/fec/crc.py:119-138 (re-encode, valid iff parity == 0)
  *   pl_gather_rows   Polar5GEncoder.forward rate matching c[:, ind_rate_matching]
  *                    my_sn/fec/polar/enc.py:378-392
  *   pl_rate_recover  Polar5GDecoder.forward rate recovery my_sn/fec/polar/dec.py:621-654
@@ -132,6 +133,9 @@ int pl_sc_source(int32_t n, const uint8_t* frozen_mask, int32_t f_mode, char* sr
  * All pointers are device pointers; rows are contiguous fp32.
  * pl_crc_attach:   out[b] = [u[b], parity(u[b])], parity bit c = XOR of g_rows[m] bit c over the
  *                  1 bits m of u[b] (g_rows: k generator rows, bit c = parity column c; degree <= 32).
+ * pl_crc_check:    valid[b] = 1 iff the parity of the whole received word[b] (len bits, g_rows: len
+ *                  generator rows) is all zero, i.e. its last degree bits are the CRC of the first
+ *                  len - degree bits; else 0.
  * pl_gather_rows:  out[b, j] = in[b, idx[j]], j < n_out <= 4096 (rate matching).
  * pl_rate_recover: out[b, j] = src_a[j] < 0 ? fill[j] : in[b, src_a[j]] (+ in[b, src_b[j]] if
  *                  src_b (nullable) has src_b[j] >= 0), j < n <= 2048 (de-interleaving, puncturing
@@ -139,6 +143,8 @@ int pl_sc_source(int32_t n, const uint8_t* frozen_mask, int32_t f_mode, char* sr
  *                  de-interleaving folded into one table). */
 int pl_crc_attach(const float* u, int64_t bs, int32_t k, const uint32_t* g_rows, int32_t degree, float* out,
                   void* hip_stream);
+int pl_crc_check(const float* word, int64_t bs, int32_t len, const uint32_t* g_rows, int32_t degree,
+                 uint8_t* valid, void* hip_stream);
 int pl_gather_rows(const float* in, int64_t bs, int32_t n_in, const int32_t* idx, int32_t n_out, float* out,
                    void* hip_stream);
 int pl_rate_recover(const float* llr, int64_t bs, int32_t e, const int32_t* src_a, const int32_t* src_b,

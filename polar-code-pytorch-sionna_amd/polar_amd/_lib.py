@@ -45,6 +45,7 @@ def _declare(L):
     L.pl_sc_source.argtypes = [i32, P, i32, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
                                ctypes.c_char_p, ctypes.c_size_t]
     L.pl_crc_attach.argtypes = [P, i64, i32, P, i32, P, P]
+    L.pl_crc_check.argtypes = [P, i64, i32, P, i32, P, P]
     L.pl_gather_rows.argtypes = [P, i64, i32, P, i32, P, P]
     L.pl_rate_recover.argtypes = [P, i64, i32, P, P, P, i32, P, P]
     L.pl_awgn_qpsk_llr.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, i64, i64, ctypes.c_float, P, P, P]
@@ -57,7 +58,7 @@ def _declare(L):
     L.pl_version.restype = ctypes.c_char_p
     for f in (L.pl_plan_create, L.pl_plan_destroy, L.pl_plan_info, L.pl_plan_device, L.pl_sc_decode, L.pl_scl_decode,
               L.pl_polar_encode, L.pl_plan_kernel, L.pl_sc_specialize, L.pl_sc_source, L.pl_plan_set_crc,
-              L.pl_crc_attach,
+              L.pl_crc_attach, L.pl_crc_check,
               L.pl_gather_rows, L.pl_rate_recover, L.pl_awgn_qpsk_llr, L.pl_count_errors,
               L.pl_awgn_qpsk_llr_bits, L.pl_sc_decode_count):
         f.restype = ctypes.c_int
@@ -81,7 +82,7 @@ def lib():
 EXPORTED_SYMBOLS = ("pl_plan_create", "pl_plan_destroy", "pl_plan_info", "pl_plan_device", "pl_sc_decode",
                     "pl_scl_workspace_size", "pl_scl_decode", "pl_polar_encode",
                     "pl_plan_kernel", "pl_sc_specialize", "pl_sc_source", "pl_plan_set_crc", "pl_crc_attach",
-                    "pl_gather_rows",
+                    "pl_crc_check", "pl_gather_rows",
                     "pl_rate_recover", "pl_awgn_qpsk_llr", "pl_count_errors", "pl_awgn_qpsk_llr_bits",
                     "pl_sc_count_workspace_size", "pl_sc_decode_count", "pl_last_error_string", "pl_version")
 

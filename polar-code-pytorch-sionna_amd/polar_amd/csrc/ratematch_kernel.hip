@@ -85,6 +85,25 @@ __global__ __launch_bounds__(kThreads) void crc_attach_kernel(const float* __res
     if (lane < degree) y[k + lane] = (float)((acc >> lane) & 1u);
 }
 
+// CRCDecoder.forward (crc.py:119-138): the reference re-encodes the whole received word
+// [info, parity] with the generator of its full length and calls it valid iff every parity bit
+// of that is 0 (for a cyclic code: the received parity equals the CRC of the info bits).  One
+// wave per word, the same row XOR as crc_attach_kernel over all len bits; one byte per word out.
+__global__ __launch_bounds__(kThreads) void crc_check_kernel(const float* __restrict__ word, int64_t bs, int len,
+                                                             const uint32_t* __restrict__ g_rows,
+                                                             uint8_t* __restrict__ valid) {
+    const int lane = threadIdx.x & 63;
+    const int64_t b = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    if (b >= bs) return;
+    const float* x = word + b * len;
+    uint32_t acc = 0u;
+    for (int m = lane; m < len; m += 64)
+        if (x[m] != 0.0f) acc ^= g_rows[m];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) acc ^= (uint32_t)__shfl_xor((int)acc, off, 64);
+    if (lane == 0) valid[b] = acc == 0u ? 1 : 0;
+}
+
 int rows_per_block(int64_t bs) {
     // >= 4 blocks per CU's worth of rows, at most 8 rows per block
     int64_t r = bs / (256 * 8);
@@ -148,6 +167,23 @@ int pl_crc_attach(const float* u, int64_t bs, int32_t k, const uint32_t* g_rows,
     hipLaunchKernelGGL(crc_attach_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
                        u, bs, k, g_rows, degree, out);
     return pl::check_hip(hipGetLastError(), "pl_crc_attach launch");
+}
+
+int pl_crc_check(const float* word, int64_t bs, int32_t len, const uint32_t* g_rows, int32_t degree,
+                 uint8_t* valid, void* stream) {
+    if (bs < 0 || len < degree || degree < 1 || degree > 32 || (bs > 0 && (!word || !g_rows || !valid))) {
+        pl::set_error("pl_crc_check: bad arguments");
+        return PL_EINVAL;
+    }
+    if (bs == 0) return PL_OK;
+    const int64_t blocks = (bs + kThreads / 64 - 1) / (kThreads / 64);
+    if (blocks > 0x7fffffffLL) {
+        pl::set_error("pl_crc_check: batch too large");
+        return PL_EINVAL;
+    }
+    hipLaunchKernelGGL(crc_check_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
+                       word, bs, len, g_rows, valid);
+    return pl::check_hip(hipGetLastError(), "pl_crc_check launch");
 }
 
 }  // extern "C"

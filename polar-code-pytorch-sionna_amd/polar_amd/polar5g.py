@@ -1,6 +1,7 @@
 """5G NR polar coding wrapper: drop-ins for my_sn/fec/polar
 
   generate_5g_ranking  <-> my_sn/fec/polar/utils.py:6-71   (3GPP TS 38.212 Table 5.3.1.2-1)
+  generate_rm_code     <-> my_sn/fec/polar/utils.py:73-101  (Reed-Muller frozen set)
   PolarEncoder         <-> my_sn/fec/polar/enc.py:7-114     (mother-code encoder)
   Polar5GEncoder       <-> my_sn/fec/polar/enc.py:115-392   (CRC, rate matching, interleavers)
   Polar5GDecoder       <-> my_sn/fec/polar/dec.py:539-666   (rate recovery, SC / CRC-aided SCL)
@@ -23,6 +24,7 @@ Differences from the reference, where it cannot run as shipped:
     argument, dec.py:587-590); here it raises NotImplementedError.
 """
 import ctypes
+import math
 import os
 
 import numpy as np
@@ -30,6 +32,7 @@ import torch as tc
 from torch import nn
 
 from . import _lib, mysn, ops
+from .crc import CRCEncoder
 from .decoders import _gpu_for
 
 _DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "polar5g_ranking.npy")
@@ -75,6 +78,21 @@ def generate_5g_ranking(k, n, sort=True, strict=True):
         info_pos = np.sort(info_pos)
         frozen_pos = np.sort(frozen_pos)
     return [frozen_pos.astype(int), info_pos.astype(int)]
+
+
+def generate_rm_code(r, m):
+    """[frozen_pos, info_pos, n, k, d_min] of the (r, m) Reed-Muller code as a polar code
+    (utils.py:73-101): the rows of F2^{(x)m} whose index has binary weight < m - r are frozen."""
+    assert r <= m, "order r cannot be larger than m."
+    n = 2 ** m
+    d_min = 2 ** (m - r)
+    k = sum(math.comb(m, i) for i in range(r + 1))
+    w = np.array([bin(i).count("1") for i in range(n)])
+    frozen_vec = w < m - r
+    frozen_pos = np.arange(n)[frozen_vec]
+    info_pos = np.arange(n)[~frozen_vec]
+    assert len(info_pos) == k, "Error: resulting k is inconsistent."
+    return frozen_pos, info_pos, n, k, d_min
 
 
 def subblock_interleaving(u):
@@ -269,7 +287,8 @@ class Polar5GEncoder(PolarEncoder):
         self._ind_input_int = idx_input
         self._crc_degree = crc_pol
         self._crc_length = mysn.crc_params(crc_pol)[0]
-        self._g_rows = crc_generator_rows(crc_pol, k)
+        self._enc_crc = CRCEncoder(crc_pol, k, dtype=dtype, device=device)  # enc.py:156
+        self._g_rows = self._enc_crc.g_rows
         self._dev_tables = {}
         if verbose:
             print(f"Code params after rate-matching: k = {k}, n = {n}")
@@ -280,7 +299,8 @@ class Polar5GEncoder(PolarEncoder):
 
     @property
     def enc_crc(self):
-        return self
+        """The CRC encoder (polar_amd.crc.CRCEncoder, enc.py:156-158)."""
+        return self._enc_crc
 
     @property
     def crc_degree(self):
