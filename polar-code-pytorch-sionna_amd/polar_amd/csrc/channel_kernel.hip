@@ -51,8 +51,6 @@ __device__ __forceinline__ U4 philox(U4 c, uint32_t k0, uint32_t k1) {
     return c;
 }
 
-// uniform in (0, 1): 24 random bits, centred in their bucket (never 0, never 1)
-__device__ __forceinline__ float unit(uint32_t v) { return ((float)(v >> 8) + 0.5f) * (1.0f / 16777216.0f); }
 
 __device__ __forceinline__ uint32_t span_mask(int h) {
     switch (h) {
@@ -64,11 +62,66 @@ __device__ __forceinline__ uint32_t span_mask(int h) {
     }
 }
 
+// Parallel bit deposit: bit i of x goes to the position of the i-th set bit of m (Hacker's
+// Delight 7-5, "expand"), five log-steps instead of a loop over the set bits (no divergence).
+__device__ __forceinline__ uint32_t expand_bits(uint32_t x, uint32_t m) {
+    const uint32_t m0 = m;
+    uint32_t mk = ~m << 1, mv[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        uint32_t mp = mk ^ (mk << 1);
+        mp ^= mp << 2;
+        mp ^= mp << 4;
+        mp ^= mp << 8;
+        mp ^= mp << 16;
+        mv[i] = mp & m;
+        m = (m ^ mv[i]) | (mv[i] >> (1 << i));
+        mk &= ~mp;
+    }
+#pragma unroll
+    for (int i = 4; i >= 0; --i) x = (x & ~mv[i]) | ((x << (1 << i)) & mv[i]);
+    return x & m0;
+}
+
 // Philox block b of a row's stream in domain d (0: information bits, 1: noise)
 __device__ __forceinline__ U4 stream_block(uint32_t k0, uint32_t k1, int64_t row, uint32_t it, uint32_t d, uint32_t b) {
     return philox(U4{(uint32_t)row, (uint32_t)(row >> 32), it, (d << 31) | b}, k0, k1);
 }
 __device__ __forceinline__ uint32_t comp(const U4& r, int c) { return c == 0 ? r.x : c == 1 ? r.y : c == 2 ? r.z : r.w; }
+
+// Constants of the logit map: logit = a_s + rs * cos/sin(angle), a_s = +-scale/sqrt(2) by the code
+// bit, rs = radius * scale * sqrt(no/2) (the radius' sqrt(2 ln 2) folded into rsc).
+struct Logit {
+    float a;    // scale / sqrt(2)
+    float rsc;  // scale * sqrt(no / 2) * sqrt(2 ln 2)
+};
+
+// Four logits from one Philox block and the four code bits in bits 0..3 of `bits`.  Box-Muller on
+// the hardware transcendentals (a noise draw, not a decoder value: only its distribution is
+// specified):
+//   radius  sqrt(-2 ln u) = sqrt(2 ln 2) sqrt(32 - log2 v'), v' = float(v | 1) in [1, 2^32], i.e.
+//           u = v' 2^-32 in (0, 1] (tail to 6.66 sigma), v_log_f32 on a normal argument;
+//   angle   v_sin / v_cos take revolutions and are periodic: the mantissa bits of v under the
+//           exponent of 1.0 give 1 + t, t uniform in [0, 1), and sin(2 pi (1 + t)) = sin(2 pi t).
+__device__ __forceinline__ float4 logits4(const U4& rnd, uint32_t bits, const Logit& lc) {
+#if PL_AWGN_DIAG == 2
+    const float c0 = (float)rnd.x, s0 = (float)rnd.y, c1 = (float)rnd.z, s1 = 1.0f, rs0 = lc.rsc, rs1 = lc.rsc;
+#else
+    const float rs0 = lc.rsc * __builtin_amdgcn_sqrtf(32.0f - __builtin_amdgcn_logf((float)(rnd.x | 1u)));
+    const float rs1 = lc.rsc * __builtin_amdgcn_sqrtf(32.0f - __builtin_amdgcn_logf((float)(rnd.z | 1u)));
+    const float t0 = __uint_as_float(0x3F800000u | (rnd.y >> 9)), t1 = __uint_as_float(0x3F800000u | (rnd.w >> 9));
+    const float c0 = __builtin_amdgcn_cosf(t0), s0 = __builtin_amdgcn_sinf(t0);
+    const float c1 = __builtin_amdgcn_cosf(t1), s1 = __builtin_amdgcn_sinf(t1);
+#endif
+    // (1 - 2 c) a: the code bit moved to the sign of a
+    const uint32_t au = __float_as_uint(lc.a);
+    const float a0 = __uint_as_float(au ^ ((bits << 31) & 0x80000000u));
+    const float a1 = __uint_as_float(au ^ ((bits << 30) & 0x80000000u));
+    const float a2 = __uint_as_float(au ^ ((bits << 29) & 0x80000000u));
+    const float a3 = __uint_as_float(au ^ ((bits << 28) & 0x80000000u));
+    return float4{__builtin_fmaf(rs0, c0, a0), __builtin_fmaf(rs0, s0, a1), __builtin_fmaf(rs1, c1, a2),
+                  __builtin_fmaf(rs1, s1, a3)};
+}
 
 // A wave holds cpw = 64 / wpc codewords (wpc = max(1, n/32) lanes per codeword).  Three phases:
 //   A  lane w < nq of a group: stream word w (32 information bits, ranks 32w .. 32w+31) -> LDS;
@@ -77,7 +130,11 @@ __device__ __forceinline__ uint32_t comp(const U4& r, int c) { return c == 0 ? r
 //   C  the whole wave over the wave's rows in chunks of CH = min(4, n) positions ("chunk layout",
 //      consecutive lanes -> consecutive chunks, so the fp32 rows are written as whole lines):
 //      u rows from the stream words, logit rows from the code bits and one Philox block per chunk.
-constexpr int kWordsPerWave = 256;  // LDS words per wave: stream words (<= 128) + code words (64)
+constexpr int kWordsPerWave = 256;
+#ifndef PL_AWGN_DIAG
+#define PL_AWGN_DIAG 0  // development only (tools/micro/producer_cost.hip): 1 no logit stores,
+                        // 2 no noise (Philox + Box-Muller), 3 no Philox for the noise
+#endif  // LDS words per wave: stream words (<= 128) + code words (64)
 
 __global__ __launch_bounds__(256) void awgn_llr_kernel(int64_t bs, int64_t row0, uint32_t k0, uint32_t k1, uint32_t it,
                                                        float no, const uint32_t* __restrict__ frozen_words, int n, int k,
@@ -118,14 +175,8 @@ __global__ __launch_bounds__(256) void awgn_llr_kernel(int64_t bs, int64_t row0,
         const int q0 = base >> 5, sh = base & 31;
         const uint32_t lo = srow[q0];
         const uint32_t hi = q0 + 1 < nq ? srow[q0 + 1] : 0u;
-        uint64_t bits = (((uint64_t)hi << 32) | lo) >> sh;  // the next (up to 32) information bits
-        uint32_t m = info;
-        while (m) {  // deposit them at the information positions, in order
-            const int j = __builtin_ctz(m);
-            x |= (uint32_t)(bits & 1u) << j;
-            bits >>= 1;
-            m &= m - 1;
-        }
+        // the next (up to 32) information bits, deposited at the information positions in order
+        x = expand_bits((uint32_t)((((uint64_t)hi << 32) | lo) >> sh), info);
     }
     for (int h = 1; h < nb; h <<= 1) x ^= (x >> h) & span_mask(h);  // x = u G_n (my_sn enc.py:85-96)
     for (int hw = 1; hw < wpc; hw <<= 1) {
@@ -167,31 +218,43 @@ __global__ __launch_bounds__(256) void awgn_llr_kernel(int64_t bs, int64_t row0,
     // C2: logits.  QPSK component of code bit j: (1 - 2 c_j)/sqrt(2) plus sqrt(no) * N(0, 1/2)
     // (awgn.py:24-29, utils.py:11-15); logit = -2 sqrt(2) y / no.  Chunk c of a row = positions
     // [CH c, CH c + CH) draws noise block c (4 uniforms -> 2 Box-Muller pairs).
-    const float sn = sqrtf(no) * 0.70710677f, a = 0.70710677f, scale = -2.8284271f / no;
+    const float scale = -2.8284271f / no;
+    const Logit lc{scale * 0.70710677f, scale * sqrtf(no) * 0.70710677f * 1.17741002f};  // sqrt(2 ln 2)
     const int CH = n >= 4 ? 4 : n, nch = n / CH, lnch = __builtin_ctz(nch);  // n is a power of two
     const bool vec = CH == 4 && ((reinterpret_cast<uintptr_t>(llr_out) & 15) == 0);
+    if (vec && nch >= 64) {
+        // rows outer (the row, hence the first Philox products, uniform across the wave), the
+        // wave's lanes over the row's chunks: one 1-KiB float4 store per instruction
+        for (int r = 0; r < rows; ++r) {
+            const int64_t grow = row0 + b0 + r;
+            const uint32_t* cw = cwd + r * wpc;
+            float4* o = reinterpret_cast<float4*>(llr_out + (b0 + r) * n);
+            for (int ch = lane; ch < nch; ch += 64) {
+#if PL_AWGN_DIAG == 3
+                const U4 rnd = U4{(uint32_t)ch * 0x9E3779B9u, (uint32_t)ch * 0x85EBCA6Bu, (uint32_t)ch * 0xC2B2AE35u,
+                                  (uint32_t)ch * 0x27D4EB2Fu};
+#else
+                const U4 rnd = stream_block(k0, k1, grow, it, 1, (uint32_t)ch);
+#endif
+                const float4 l = logits4(rnd, cw[ch >> 3] >> ((ch & 7) * 4), lc);
+#if PL_AWGN_DIAG == 1
+                if (l.x + l.y + l.z + l.w != 1234.5f) continue;
+#endif
+                o[ch] = l;
+            }
+        }
+        return;
+    }
     for (int c = lane; c < rows * nch; c += 64) {
         const int r = c >> lnch, ch = c & (nch - 1), p = ch * CH;
         const U4 rnd = stream_block(k0, k1, row0 + b0 + r, it, 1, (uint32_t)ch);
-        // Box-Muller on the hardware transcendentals: the uniforms lie in [2^-25, 1), so v_log_f32
-        // (log2) needs no denormal scaling; v_sin/v_cos take revolutions, sin(2 pi u) = v_sin(u).
-        // (A noise draw, not a decoder value: only its distribution is specified.)
-        const float ln2 = 0.69314718f;
-        const float r0 = __builtin_amdgcn_sqrtf(-2.0f * ln2 * __builtin_amdgcn_logf(unit(rnd.x)));
-        const float r1 = __builtin_amdgcn_sqrtf(-2.0f * ln2 * __builtin_amdgcn_logf(unit(rnd.z)));
-        const float ty = unit(rnd.y), tw = unit(rnd.w);
-        const float z[4] = {r0 * __builtin_amdgcn_cosf(ty), r0 * __builtin_amdgcn_sinf(ty),
-                            r1 * __builtin_amdgcn_cosf(tw), r1 * __builtin_amdgcn_sinf(tw)};
-        const uint32_t bits = cwd[r * wpc + (p >> 5)] >> (p & 31);
-        float l[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)  // (1 - 2 c) a: the code bit moved to the sign of a
-            l[i] = scale * (__uint_as_float(__float_as_uint(a) ^ ((bits << (31 - i)) & 0x80000000u)) + sn * z[i]);
+        const float4 l = logits4(rnd, cwd[r * wpc + (p >> 5)] >> (p & 31), lc);
         float* o = llr_out + (b0 + r) * n + p;
         if (vec) {
-            *reinterpret_cast<float4*>(o) = float4{l[0], l[1], l[2], l[3]};
+            *reinterpret_cast<float4*>(o) = l;
         } else {
-            for (int i = 0; i < CH; ++i) o[i] = l[i];
+            const float lv[4] = {l.x, l.y, l.z, l.w};
+            for (int i = 0; i < CH; ++i) o[i] = lv[i];
         }
     }
 }
