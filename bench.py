@@ -98,8 +98,9 @@ def sim_iteration(plan, fp, k, n, bs, ebno, dev, reps=20):
     """One Monte-Carlo iteration of the harness on this GPU, measured
     after the timed region: the fused producer (pl_awgn_qpsk_llr: bits, encoder, QPSK, AWGN,
     logits), the SC decode and the error counter (pl_count_errors), each by HIP events; and the
-    path sim_ber takes for FusedAWGN + SC_Dec (pl_awgn_qpsk_llr_bits, packed bits, then
-    pl_sc_decode_count: decode and count in one kernel, no bit rows), timed as whole iterations."""
+    two fused paths of FusedAWGN.error_counts, timed as whole iterations: pl_awgn_qpsk_llr_bits +
+    pl_sc_decode_count (packed bits, decode and count in one kernel, no bit rows) and
+    pl_sc_sim_count (the whole iteration inside the SC kernel, sim_ber's default path)."""
     from polar_amd import _lib, channel, ops
     enc = _lib.Plan(n, plan_mask(fp, n), 1, flags=_lib.PL_PLAN_GENERIC, device=dev)
     no = float(channel.ebnodb2no(ebno, 2, k / n))
@@ -138,7 +139,32 @@ def sim_iteration(plan, fp, k, n, bs, ebno, dev, reps=20):
         torch.cuda.synchronize(dev)
         ms = e0.elapsed_time(e1) / reps
         res["decode_count_path"] = {"mcw_s": round(bs / ms / 1e3, 2), "iteration_ms": round(ms, 5),
-                                    "note": "pl_awgn_qpsk_llr_bits + pl_sc_decode_count (sim_ber's path)"}
+                                    "note": "pl_awgn_qpsk_llr_bits + pl_sc_decode_count"}
+        try:
+            ops.sc_sim_count(plan, bs, no, 42, 0, 0, counts)
+        except _lib.PolarLibError:
+            return res
+        ws_bytes = int(_lib.lib().pl_sc_count_workspace_size(plan.handle, bs))
+        ws = torch.empty((ws_bytes,), dtype=torch.uint8, device=dev)
+        import ctypes
+        L = _lib.lib()
+
+        def sim_iter(i):
+            _lib.check(L.pl_sc_sim_count(plan.handle, 42, i, 0, bs, no, ctypes.c_void_p(counts.data_ptr()),
+                                         ctypes.c_void_p(ws.data_ptr()), ws_bytes, None, None,
+                                         _lib.current_stream_ptr(dev)), "pl_sc_sim_count")
+        sim_iter(1)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for i in range(reps):
+            sim_iter(2 + i)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1) / reps
+        res["sim_kernel_path"] = {"mcw_s": round(bs / ms / 1e3, 2), "iteration_ms": round(ms, 5),
+                                  "note": "pl_sc_sim_count: bits, encoder, QPSK, AWGN, logits, SC decode and "
+                                          "error count in one kernel, nothing but the counters in HBM "
+                                          "(sim_ber's path)"}
     return res
 
 

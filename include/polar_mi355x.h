@@ -169,7 +169,17 @@ int pl_rate_recover(const float* llr, int64_t bs, int32_t e, const int32_t* src_
  *                  accumulates counts[0] += bit errors, counts[1] += block errors (int64 device
  *                  counters) -- pl_sc_decode + pl_count_errors in one pass (sim.py:84-100).
  *                  workspace: pl_sc_count_workspace_size(plan, bs) bytes of device scratch.
- *                  PL_ENOTSUP for plans on the generic SC kernel (pl_plan_kernel: 0). */
+ *                  PL_ENOTSUP for plans on the generic SC kernel (pl_plan_kernel: 0).
+ * pl_sc_sim_count: one whole Monte-Carlo iteration of the harness (System_AWGN_model.forward,
+ *                  awgn_model.py:33-44, then sim.py:84-100's counters) in the SC kernel itself:
+ *                  information bits, polar encoding, QPSK, AWGN and logits are generated in the
+ *                  decoder's lane layout (Philox4x32-10 keyed by seed, counter (row0 + row,
+ *                  iteration, stream word); streams distinct from pl_awgn_qpsk_llr's), decoded, and
+ *                  compared in registers: counts[0] += bit errors, counts[1] += block errors.  No
+ *                  LLR or bit row is written unless llr_dump ([bs, n] fp32 logits) / u_dump ([bs, k]
+ *                  fp32 information bits) are given (nullable; for tests).  workspace as
+ *                  pl_sc_decode_count.  PL_ENOTSUP unless the plan's specialised kernel has 64
+ *                  channel slots per lane (min-sum n = 64 ... 1024; pl_plan_kernel: 1). */
 int pl_awgn_qpsk_llr(const pl_plan* plan, uint64_t seed, uint64_t iteration, int64_t row0, int64_t bs, float no,
                      float* u_out, float* llr_out, void* hip_stream);
 int pl_awgn_qpsk_llr_bits(const pl_plan* plan, uint64_t seed, uint64_t iteration, int64_t row0, int64_t bs,
@@ -178,6 +188,9 @@ int pl_count_errors(const float* a, const float* b, int64_t rows, int32_t k, int
 size_t pl_sc_count_workspace_size(const pl_plan* plan, int64_t bs);
 int pl_sc_decode_count(const pl_plan* plan, const float* llr_logits, int64_t bs, const uint32_t* ref_bits,
                        int64_t* counts, void* workspace, size_t ws_bytes, void* hip_stream);
+int pl_sc_sim_count(const pl_plan* plan, uint64_t seed, uint64_t iteration, int64_t row0, int64_t bs, float no,
+                    int64_t* counts, void* workspace, size_t ws_bytes, float* llr_dump, float* u_dump,
+                    void* hip_stream);
 
 const char* pl_last_error_string(void);
 const char* pl_version(void);

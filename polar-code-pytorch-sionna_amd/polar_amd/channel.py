@@ -207,8 +207,10 @@ class FusedAWGN(nn.Module):
     keyed by `seed`; every call draws a fresh iteration of the stream (`iteration` counts calls),
     and `row0` offsets the rows (a rank's shard of a multi-GPU batch)."""
 
-    def __init__(self, n, k, frozen_pos, decoder, device=None, seed=42, row0=0, cw_estimates=False):
+    def __init__(self, n, k, frozen_pos, decoder, device=None, seed=42, row0=0, cw_estimates=False,
+                 sim_kernel=True):
         super().__init__()
+        self.sim_kernel = bool(sim_kernel)  # error_counts: the fused producer+decoder kernel when the plan has it
         from . import _lib
         from .frozen import frozen_mask
         self.n, self.k = int(n), int(k)
@@ -244,13 +246,17 @@ class FusedAWGN(nn.Module):
 
     def error_counts(self, batch_size, ebno_db, counts=None):
         """One Monte-Carlo iteration straight to the harness's counters: [bit errors, block errors]
-        (int64 [2] on the device, accumulated into counts) of decoding this iteration's batch --
-        what count_errors / count_block_errors (my_sn/sim.py:7-18) give on forward()'s output, for
-        the same draw.  The producer writes the information bits packed (pl_awgn_qpsk_llr_bits) and
-        the specialised SC kernel compares its decisions with them instead of writing bit rows
-        (pl_sc_decode_count).  Returns None (nothing drawn) when the decoder is not this package's
-        SC_Dec on a specialised plan; sim_ber then runs forward() and counts separately."""
-        from . import ops
+        (int64 [2] on the device, accumulated into counts) of decoding a fresh batch -- what
+        count_errors / count_block_errors (my_sn/sim.py:7-18) give on forward()'s output.
+          * pl_sc_sim_count (sim_kernel=True and a specialised plan with 64 channel slots per
+            lane): the whole iteration inside the SC kernel, nothing written to HBM but the
+            counters; its Philox streams are its own (the same model, not forward()'s draw).
+          * otherwise pl_awgn_qpsk_llr_bits + pl_sc_decode_count: the producer writes the logits
+            and the information bits packed, the decoder compares its decisions with them -- the
+            same draw as forward() for this iteration.
+        Returns None (nothing drawn) when the decoder is not this package's SC_Dec on a specialised
+        plan; sim_ber then runs forward() and counts separately."""
+        from . import _lib, ops
         from .decoders import SC_Dec
         dec = self.decoder
         if self.cw_estimates or type(dec) is not SC_Dec or dec.mode not in ("llr", "max"):
@@ -261,6 +267,13 @@ class FusedAWGN(nn.Module):
         no = float(ebnodb2no(float(ebno_db), self.n_bits_per_sym, self.coderate))
         it = self.iteration
         self.iteration += 1
+        if self.sim_kernel:
+            try:
+                return ops.sc_sim_count(plan, int(batch_size), no, self.seed, it, self.row0, counts)
+            except _lib.PolarLibError as e:
+                if e.code != _lib.PL_ENOTSUP:
+                    raise
+                self.sim_kernel = False  # this plan's kernel has no fused entry: the two-kernel path
         ubits, llr = ops.awgn_qpsk_llr_bits(self._plans.get(self.device, self._make_plan), int(batch_size), no,
                                             self.seed, it, self.row0)
         return ops.sc_decode_count(plan, llr, ubits, counts)

@@ -274,6 +274,33 @@ int pl_sc_decode_count(const pl_plan* p, const float* llr, int64_t bs, const uin
     return pl::launch_sum_pairs(part, pl::sc_count_waves(p, bs), counts, st);
 }
 
+int pl_sc_sim_count(const pl_plan* p, uint64_t seed, uint64_t iteration, int64_t row0, int64_t bs, float no,
+                    int64_t* counts, void* ws, size_t ws_bytes, float* llr_dump, float* u_dump, void* stream) {
+    if (!p || bs < 0 || row0 < 0 || !counts || !(no > 0.0f)) {
+        pl::set_error("pl_sc_sim_count: bad arguments (no must be > 0)");
+        return PL_EINVAL;
+    }
+    if (p->list_size != 1) {
+        pl::set_error("pl_sc_sim_count: needs an SC plan (list_size 1)");
+        return PL_EINVAL;
+    }
+    if (!p->sc_module || !p->sc_fn_sim) {
+        pl::set_error("pl_sc_sim_count: the plan's kernel has no fused Monte-Carlo entry (generic kernel, or not "
+                      "64 channel slots per lane); use pl_awgn_qpsk_llr_bits + pl_sc_decode_count");
+        return PL_ENOTSUP;
+    }
+    if (int r = pl::check_device(p, static_cast<hipStream_t>(stream), "pl_sc_sim_count")) return r;
+    if (bs == 0) return PL_OK;
+    if (ws_bytes < pl_sc_count_workspace_size(p, bs) || !ws) {
+        pl::set_error("pl_sc_sim_count: workspace too small (pl_sc_count_workspace_size)");
+        return PL_EINVAL;
+    }
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    int32_t* part = static_cast<int32_t*>(ws);
+    if (int r = pl::launch_sc_static_sim(p, seed, iteration, row0, bs, no, part, llr_dump, u_dump, st)) return r;
+    return pl::launch_sum_pairs(part, pl::sc_count_waves(p, bs), counts, st);
+}
+
 size_t pl_scl_workspace_size(const pl_plan* p, int64_t bs) { return p ? pl::scl_workspace_size(p, bs) : 0; }
 
 int pl_scl_decode(const pl_plan* p, const float* llr, int64_t bs, void* out, int32_t out_kind, double* out_pm,

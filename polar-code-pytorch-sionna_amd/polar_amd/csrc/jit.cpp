@@ -174,6 +174,8 @@ std::string static_source(int n, const uint8_t* frozen, int f_mode) {
     std::ostringstream o;
     o << "// pl-genco-flags: " << kGencoFlags << "\n// pl-compiler: " << __clang_version__ << "\n";
     if (tuned_wide(log_n, f_mode)) o << "#define PL_SC_MINW 3\n#define PL_SC_F_BITOP3 1\n";
+    const int G = 1 << lg, NS = n >> lg;
+    if (NS == 64) o << "#define PL_SC_SIM 1\n";  // the fused Monte-Carlo entry (sc_static.h OUT_SIM)
     // PL_SC_DEFINES="NAME=VALUE ..." overrides the kernel's tuning macros (development variants;
     // part of the source, hence of the cache key)
     if (const char* defs = getenv("PL_SC_DEFINES")) {
@@ -196,7 +198,19 @@ std::string static_source(int n, const uint8_t* frozen, int f_mode) {
       << ", LOG_G = " << lg << ", G = " << (1 << lg) << ", NS = " << (n >> lg) << ", FM = " << f_mode
       << ";\n  static constexpr unsigned char NT[" << nt.size() << "] = {";
     for (size_t i = 0; i < nt.size(); ++i) o << (i ? "," : "") << (int)nt[i];
-    o << "};\n};\nPL_SC_STATIC_KERNELS(PlCode)\n";
+    o << "};\n";
+    if (NS == 64) {
+        // INFO_LANE[r]: bit j = position r + G j is an information position
+        o << "  static constexpr unsigned long long INFO_LANE[" << G << "] = {";
+        for (int r = 0; r < G; ++r) {
+            unsigned long long m = 0;
+            for (int j = 0; j < 64; ++j)
+                if (!frozen[r + G * j]) m |= 1ull << j;
+            o << (r ? "," : "") << m << "ull";
+        }
+        o << "};\n";
+    }
+    o << "};\nPL_SC_STATIC_KERNELS(PlCode)\n";
     return o.str();
 }
 
@@ -286,6 +300,11 @@ int attach_static(pl_plan* p, const uint8_t* frozen, bool allow_compile) {
         cnt = nullptr;
         (void)hipGetLastError();
     }
+    hipFunction_t sim = nullptr;  // optional (codes with 64 slots per lane): producer + decode + count
+    if (!r && hipModuleGetFunction(&sim, mod, "pl_sc_static_sim") != hipSuccess) {
+        sim = nullptr;
+        (void)hipGetLastError();
+    }
     // info_loc[m]: where the u bit of information position m sits in a wave's LDS u words
     // (sc_static.h emit): (byte offset of its word in codeword 0's area) << 5 | bit in the word
     const int lg = static_log_g(p->log_n, p->f_mode);
@@ -327,6 +346,7 @@ int attach_static(pl_plan* p, const uint8_t* frozen, bool allow_compile) {
     p->sc_fn_f32 = f32;
     p->sc_fn_u8 = u8;
     p->sc_fn_cnt = cnt;
+    p->sc_fn_sim = sim;
     p->kernel_path = path;
     return PL_OK;
 }
@@ -334,7 +354,7 @@ int attach_static(pl_plan* p, const uint8_t* frozen, bool allow_compile) {
 void detach_static(pl_plan* p) {
     if (p->sc_module) (void)hipModuleUnload(p->sc_module);
     p->sc_module = nullptr;
-    p->sc_fn_f32 = p->sc_fn_u8 = p->sc_fn_cnt = nullptr;
+    p->sc_fn_f32 = p->sc_fn_u8 = p->sc_fn_cnt = p->sc_fn_sim = nullptr;
 }
 
 int64_t sc_count_waves(const pl_plan* p, int64_t bs) {
@@ -360,6 +380,24 @@ int launch_sc_static_count(const pl_plan* p, const float* llr, int64_t bs, const
     void* args[] = {(void*)&llr, (void*)&bs, (void*)&part, (void*)&loc, (void*)&k, (void*)&lmax, (void*)&ref};
     return check_hip(hipModuleLaunchKernel(p->sc_fn_cnt, (unsigned)blocks, 1, 1, 256, 1, 1, 0, st, args, nullptr),
                      "SC decode+count launch (specialised)");
+}
+
+int launch_sc_static_sim(const pl_plan* p, uint64_t seed, uint64_t iteration, int64_t row0, int64_t bs, float no,
+                         int32_t* part, float* llr_dump, float* u_dump, hipStream_t st) {
+    if (bs == 0) return PL_OK;
+    const int64_t blocks = sc_count_waves(p, bs) / 4;
+    if (blocks > 0x7fffffffLL) {
+        set_error("SC Monte-Carlo iteration: batch too large for one launch");
+        return PL_EINVAL;
+    }
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32), it = (uint32_t)iteration;
+    const float lmax = p->llr_max;
+    int k = p->k;
+    const int32_t* loc = p->d_info_loc;
+    void* args[] = {(void*)&bs,  (void*)&row0, (void*)&k0, (void*)&k1,   (void*)&it,       (void*)&no,
+                    (void*)&part, (void*)&loc, (void*)&k,  (void*)&lmax, (void*)&llr_dump, (void*)&u_dump};
+    return check_hip(hipModuleLaunchKernel(p->sc_fn_sim, (unsigned)blocks, 1, 1, 256, 1, 1, 0, st, args, nullptr),
+                     "SC Monte-Carlo iteration launch (specialised)");
 }
 
 int launch_sc_static(const pl_plan* p, const float* llr, int64_t bs, void* out, int out_kind, hipStream_t st) {

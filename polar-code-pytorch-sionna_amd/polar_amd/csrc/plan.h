@@ -22,6 +22,7 @@ struct pl_plan {
     hipModule_t sc_module = nullptr;
     hipFunction_t sc_fn_f32 = nullptr, sc_fn_u8 = nullptr;
     hipFunction_t sc_fn_cnt = nullptr;   // decode + error count (pl_sc_decode_count); null if absent
+    hipFunction_t sc_fn_sim = nullptr;   // producer + decode + count (pl_sc_sim_count); null if absent
     std::string kernel_path;             // code object the module came from
     int32_t crc_deg = 0;                 // SCL CRC-aided pick: degree (0 = none) and generator
     uint32_t crc_g = 0;                  //   mask without the leading term
@@ -60,6 +61,8 @@ int launch_sc_static(const pl_plan* plan, const float* llr, int64_t bs, void* ou
 int64_t sc_count_waves(const pl_plan* plan, int64_t bs);
 int launch_sc_static_count(const pl_plan* plan, const float* llr, int64_t bs, const uint32_t* ref, int32_t* part,
                            hipStream_t stream);
+int launch_sc_static_sim(const pl_plan* plan, uint64_t seed, uint64_t iteration, int64_t row0, int64_t bs, float no,
+                         int32_t* part, float* llr_dump, float* u_dump, hipStream_t stream);
 // counts[0..1] += the sums of the [bit, block] pairs of part (channel_kernel.hip)
 int launch_sum_pairs(const int32_t* part, int64_t pairs, int64_t* counts, hipStream_t stream);
 }  // namespace pl

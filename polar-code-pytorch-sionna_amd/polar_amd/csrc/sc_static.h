@@ -118,7 +118,7 @@ typedef unsigned long uintptr_t;
 namespace pls {
 
 enum : int { R0 = 0, R1 = 1, REP = 2, SPC = 3, GEN = 4 };
-enum : int { OUT_F32 = 0, OUT_U8 = 1, OUT_CNT = 2 };
+enum : int { OUT_F32 = 0, OUT_U8 = 1, OUT_CNT = 2, OUT_SIM = 3 };
 constexpr int kWaves = 4;  // waves per workgroup
 
 template <bool B, class T, class F>
@@ -726,11 +726,11 @@ __device__ __forceinline__ void lane_layout(int q, int& res, uint32_t (&lom)[5])
 }
 
 
-// u = x * G_n (G_n is an involution): in-lane spans on the packed slots, then the cross-lane
-// spans with the mirror DPP (the low element of each pair takes the XOR).  Writes this lane's
-// u words to its LDS slot.
+// u = x * G_n (G_n is an involution; the same transform encodes, x = u * G_n): in-lane spans on
+// the packed slots, then the cross-lane spans with the mirror DPP (the low element of each pair
+// takes the XOR).  w[0 .. WPL) = this lane's words (slot j = bit j % 32 of word j / 32).
 template <class C>
-__device__ __forceinline__ void to_u(uint64_t lo, uint64_t hi, const Lane& ln, uint32_t* __restrict__ mine) {
+__device__ __forceinline__ void butterfly(uint64_t lo, uint64_t hi, const Lane& ln, uint32_t (&w)[4]) {
     constexpr int NS = C::NS, LG = C::LOG_G, WPL = (NS + 31) / 32;
     constexpr uint64_t M[6] = {0x5555555555555555ull, 0x3333333333333333ull, 0x0f0f0f0f0f0f0f0full,
                                0x00ff00ff00ff00ffull, 0x0000ffff0000ffffull, 0x00000000ffffffffull};
@@ -742,7 +742,10 @@ __device__ __forceinline__ void to_u(uint64_t lo, uint64_t hi, const Lane& ln, u
         }
     }
     if constexpr (NS > 64) lo ^= hi;
-    uint32_t w[4] = {(uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32)};
+    w[0] = (uint32_t)lo;
+    w[1] = (uint32_t)(lo >> 32);
+    w[2] = (uint32_t)hi;
+    w[3] = (uint32_t)(hi >> 32);
 #pragma unroll
     for (int i = 0; i < WPL; ++i) {
         if constexpr (LG >= 4) w[i] ^= mir<16>(w[i]) & ln.lom(4);
@@ -750,6 +753,14 @@ __device__ __forceinline__ void to_u(uint64_t lo, uint64_t hi, const Lane& ln, u
         if constexpr (LG >= 2) w[i] ^= mir<4>(w[i]) & ln.lom(2);
         if constexpr (LG >= 1) w[i] ^= mir<2>(w[i]) & ln.lom(1);
     }
+}
+
+// The root's partial sums -> this lane's u words in its LDS slot.
+template <class C>
+__device__ __forceinline__ void to_u(uint64_t lo, uint64_t hi, const Lane& ln, uint32_t* __restrict__ mine) {
+    constexpr int WPL = (C::NS + 31) / 32;
+    uint32_t w[4];
+    butterfly<C>(lo, hi, ln, w);
 #pragma unroll
     for (int i = 0; i < WPL; ++i) mine[i] = w[i];
 }
@@ -900,6 +911,130 @@ __device__ __forceinline__ void count_emit(const uint32_t* __restrict__ ubase, i
     }
 }
 
+// ---------------- OUT_SIM: the Monte-Carlo producer fused in front of the decoder ----------
+// One iteration of System_AWGN_model.forward (awgn_model.py:33-41: BinarySource, polar encoder,
+// QPSK, AWGN, demapper) generated in the decoder's own lane layout, decoded, and compared with the
+// information bits in registers (my_sn/sim.py:7-18): no LLR or bit row touches HBM.  Codes with
+// 64 slots per lane (C::NS == 64); the lane holding residue r of a codeword holds positions
+// r + G j, j < 64.  Random streams (Philox4x32-10, key = seed, counter (row, row >> 32,
+// iteration, word 3)), distinct from pl_awgn_qpsk_llr's by bit 30 of word 3:
+//   information bits  word 3 = 0x40000000 | r >> 1: position r + G j (if not frozen) = bit j % 32
+//                     of component 2 (r & 1) + j / 32 (even residues x, y; odd z, w);
+//   noise             word 3 = 0xC0000000 | (16 r + t): slots 4t .. 4t+3 of residue r, the same
+//                     Box-Muller and logit map as channel_kernel.hip logits4.
+struct SimArgs {
+    int64_t row0;  // stream row of the launch's codeword 0
+    uint32_t k0, k1, it;
+    float no;
+    float* llr_dump;  // nullable: [bs, N] fp32 logits as generated (tests)
+    float* u_dump;    // nullable: [bs, K] fp32 information bits as generated (tests)
+};
+
+struct U4s {
+    uint32_t x, y, z, w;
+};
+
+// Random123 philox4x32_R(10, ...), as channel_kernel.hip philox
+__device__ __forceinline__ U4s philox10(U4s c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c.x, p1 = (uint64_t)0xCD9E8D57u * c.z;
+        c = U4s{(uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1, (uint32_t)p0};
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+
+// channel_kernel.hip logits4: four logits from one Philox block and four code bits (bits 0..3);
+// la = scale / sqrt(2), rsc = scale * sqrt(no / 2) * sqrt(2 ln 2), scale = -2 sqrt(2) / no
+__device__ __forceinline__ void logits4(const U4s& rnd, uint32_t bits, float la, float rsc, float (&l)[4]) {
+    const float rs0 = rsc * __builtin_amdgcn_sqrtf(32.0f - __builtin_amdgcn_logf((float)(rnd.x | 1u)));
+    const float rs1 = rsc * __builtin_amdgcn_sqrtf(32.0f - __builtin_amdgcn_logf((float)(rnd.z | 1u)));
+    const float t0 = uf(0x3F800000u | (rnd.y >> 9)), t1 = uf(0x3F800000u | (rnd.w >> 9));
+    const uint32_t au = fu(la);
+    l[0] = __builtin_fmaf(rs0, __builtin_amdgcn_cosf(t0), uf(au ^ ((bits << 31) & 0x80000000u)));
+    l[1] = __builtin_fmaf(rs0, __builtin_amdgcn_sinf(t0), uf(au ^ ((bits << 30) & 0x80000000u)));
+    l[2] = __builtin_fmaf(rs1, __builtin_amdgcn_cosf(t1), uf(au ^ ((bits << 29) & 0x80000000u)));
+    l[3] = __builtin_fmaf(rs1, __builtin_amdgcn_sinf(t1), uf(au ^ ((bits << 28) & 0x80000000u)));
+}
+
+// information mask of residue `res` (bit j = position res + G j is not frozen), from the code's
+// compile-time table
+template <class C, int R = 0>
+__device__ __forceinline__ uint64_t info_lane(int res) {
+    if constexpr (R == C::G) {
+        return 0;
+    } else {
+        constexpr uint64_t m = C::INFO_LANE[R];
+        return res == R ? m : info_lane<C, R + 1>(res);
+    }
+}
+
+// The channel slots of this lane (slots >= NS/2 into its LDS rows when Ch<C>::CHL) and its
+// information bits g (slot words), generated as described above.
+template <class C>
+__device__ __forceinline__ void gen_channel(float (&chv)[C::NS], const Lane& ln, float* chl_lane, const SimArgs& sa,
+                                            int64_t cw0, int64_t bs, int lane, int res, uint32_t (&g)[2]) {
+    static_assert(C::NS == 64, "OUT_SIM: 64 slots per lane");
+    constexpr int G = C::G;
+    const int64_t cw = cw0 + (lane >> C::LOG_G);
+    const uint64_t row = (uint64_t)(sa.row0 + cw);
+    const uint32_t rlo = (uint32_t)row, rhi = (uint32_t)(row >> 32);
+    const uint64_t info = info_lane<C>(res);
+    const U4s b = philox10(U4s{rlo, rhi, sa.it, 0x40000000u | (uint32_t)(res >> 1)}, sa.k0, sa.k1);
+    g[0] = ((res & 1) ? b.z : b.x) & (uint32_t)info;
+    g[1] = ((res & 1) ? b.w : b.y) & (uint32_t)(info >> 32);
+    uint32_t x[4];
+    butterfly<C>((uint64_t)g[0] | ((uint64_t)g[1] << 32), 0, ln, x);  // code bits x = u G_n
+    const float scale = -2.8284271f / sa.no;
+    const float la = scale * 0.70710677f, rsc = scale * __builtin_sqrtf(sa.no) * (0.70710677f * 1.17741002f);
+    const bool dump = sa.llr_dump != nullptr && cw < bs;
+    float* drow = dump ? sa.llr_dump + cw * C::N + res : nullptr;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+        const U4s rnd = philox10(U4s{rlo, rhi, sa.it, 0xC0000000u | (uint32_t)(res * 16 + t)}, sa.k0, sa.k1);
+        float l[4];
+        logits4(rnd, x[t >> 3] >> ((t & 7) * 4), la, rsc, l);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int j = 4 * t + i;
+            if (Ch<C>::CHL && j >= C::NS / 2) chl_lane[(j - C::NS / 2) * 64] = l[i];
+            else chv[j] = l[i];
+        }
+        if (dump) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) drow[(4 * t + i) * G] = l[i];
+        }
+    }
+}
+
+// [bit errors, block errors] of the wave's codewords: decoded u words (from the root's partial
+// sums) against the generated ones; lane 0 stores the pair at part[2 * wid].
+template <class C>
+__device__ __forceinline__ void sim_count(uint64_t lo, uint64_t hi, const Lane& ln, const uint32_t (&g)[2], int64_t cw0,
+                                          int64_t bs, int lane, int32_t* __restrict__ part, int wid) {
+    constexpr int G = C::G, CW = 64 / G;
+    uint32_t w[4];
+    butterfly<C>(lo, hi, ln, w);
+    const bool live = cw0 + (lane >> C::LOG_G) < bs;
+    uint32_t e = live ? (uint32_t)(__builtin_popcount(w[0] ^ g[0]) + __builtin_popcount(w[1] ^ g[1])) : 0u;
+    const uint64_t bad = __builtin_amdgcn_ballot_w64(e != 0u);
+    uint32_t blocks = 0;
+    if constexpr (G == 1) {
+        blocks = (uint32_t)__builtin_popcountll(bad);
+    } else {
+#pragma unroll
+        for (int c = 0; c < CW; ++c) blocks += ((bad >> (c * G)) & ((1ull << G) - 1ull)) != 0 ? 1u : 0u;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) e += (uint32_t)__shfl_xor((int)e, off, 64);
+    if (lane == 0) {
+        part[2 * wid] = (int32_t)e;
+        part[2 * wid + 1] = (int32_t)blocks;
+    }
+}
+
 // this lane's float4-path table entries, loaded early (their latency hides behind the channel)
 template <class C>
 __device__ __forceinline__ void preload_info(const int32_t* __restrict__ info_loc, int4 (&il)[2], int lane) {
@@ -1002,8 +1137,9 @@ __device__ __forceinline__ void root_virtual(float (&chv)[C::NS], const Lane& ln
 template <class C, int OUT>
 __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs, void* __restrict__ out,
                                        const int32_t* __restrict__ info_loc, int k, float lmax,
-                                       uint32_t* __restrict__ ulds, const uint32_t* __restrict__ ref = nullptr) {
-    static_assert(OUT != OUT_CNT || (!PL_SC_PERSIST && !PL_SC_STAMPS), "OUT_CNT: plain decoder only");
+                                       uint32_t* __restrict__ ulds, const uint32_t* __restrict__ ref = nullptr,
+                                       const SimArgs* sa = nullptr) {
+    static_assert(OUT < OUT_CNT || (!PL_SC_PERSIST && !PL_SC_STAMPS && PL_SC_ROOT_MODE == 0), "OUT_CNT / OUT_SIM: plain decoder only");
     constexpr int N = C::N, G = C::G, LG = C::LOG_G, NS = C::NS, CW = 64 / G;
     constexpr int WPL = (NS + 31) / 32;
     // the wave index is wave-uniform: as an SGPR value all batch/row address math is scalar
@@ -1066,15 +1202,17 @@ __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs
 #endif
     uint64_t lo = 0, hi = 0;
     int4 il[2];
-    preload_info<C>(info_loc, il, lane);
+    if constexpr (OUT != OUT_SIM) preload_info<C>(info_loc, il, lane);
 #if PL_SC_ROOT_MODE == 0
     float chv[NS];
+    uint32_t gsim[2] = {0u, 0u};  // OUT_SIM: the generated information bits (slot words)
 #if PL_SC_DIAG_NO_LOAD  // diagnostic only (wrong results): the tree without the channel loads
 #pragma unroll
     for (int j = 0; j < NS; ++j) chv[j] = (float)((lane * 7 + j * 13) % 61) - 30.5f;
     asm volatile("" ::"v"(llr));
 #else
-    load_channel<C>(chv, llr, cw0, bs, lane, res, chl_wave);
+    if constexpr (OUT == OUT_SIM) gen_channel<C>(chv, ln, chl_wave + lane, *sa, cw0, bs, lane, res, gsim);
+    else load_channel<C>(chv, llr, cw0, bs, lane, res, chl_wave);
 #endif
 #if PL_SC_STAMPS
     __builtin_amdgcn_s_waitcnt(0);
@@ -1092,6 +1230,18 @@ __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs
 #else
     root_virtual<C>(chv, ln, lo, hi, NoHook());
 #endif
+    if constexpr (OUT == OUT_SIM) {
+        sim_count<C>(lo, hi, ln, gsim, cw0, bs, lane, static_cast<int32_t*>(out), blockIdx.x * kWaves + wave);
+        if (sa->u_dump != nullptr) {  // tests: the generated bits as fp32 rows, through the emit path
+            wave_lds_fence();
+            mine[0] = gsim[0];
+            mine[1] = gsim[1];
+            wave_lds_fence();
+            preload_info<C>(info_loc, il, lane);
+            emit<C, OUT_F32>(ubase, cw0, bs, sa->u_dump, info_loc, il, lane);
+        }
+        return;
+    }
 #else
     // Stage LOG_N-1 held in VGPRs; the channel is read once per half (the second read is
     // served by the caches) and is never live across a half's subtree.
@@ -1301,11 +1451,31 @@ __device__ __forceinline__ void decode_staged(const float* __restrict__ llr, int
         pls::decode<CODE, pls::OUT_CNT>(llr, bs, part, info_loc, k, lmax, ulds, ref);                        \
     }
 #endif
+// producer + decode + error count (pl_sc_sim_count); codes with 64 slots per lane (jit.cpp
+// defines PL_SC_SIM for those and emits the code's INFO_LANE table)
+#ifndef PL_SC_SIM
+#define PL_SC_SIM 0
+#endif
+#if !PL_SC_SIM || PL_SC_PERSIST || PL_SC_STAMPS || PL_SC_ROOT_MODE
+#define PL_SC_SIM_ENTRY(CODE)
+#else
+#define PL_SC_SIM_ENTRY(CODE)                                                                                \
+    extern "C" __global__ __launch_bounds__(64 * pls::kWaves, PL_SC_MINW) void pl_sc_static_sim(             \
+        int64_t bs, int64_t row0, uint32_t k0, uint32_t k1, uint32_t it, float no, int32_t* __restrict__ part, \
+        const int32_t* __restrict__ info_loc, int k, float lmax, float* __restrict__ llr_dump,               \
+        float* __restrict__ u_dump) {                                                                         \
+        __shared__ uint32_t ulds[pls::Ch<CODE>::CHL ? pls::kWaves * 64 * (CODE::NS / 2)                       \
+                                                    : pls::kWaves * 64 * ((CODE::NS + 31) / 32)];              \
+        const pls::SimArgs sa{row0, k0, k1, it, no, llr_dump, u_dump};                                       \
+        pls::decode<CODE, pls::OUT_SIM>(nullptr, bs, part, info_loc, k, lmax, ulds, nullptr, &sa);           \
+    }
+#endif
 #define PL_SC_STATIC_KERNELS(CODE)                                                                           \
     extern "C" __device__ const int pl_sc_persistent = PL_SC_PERSIST;                                       \
     extern "C" __device__ const int pl_sc_blocks_per_cu = PL_SC_PERSIST_BPC;                                \
     PL_SC_ENTRY(CODE, pl_sc_static_f32, pls::OUT_F32)                                                        \
     PL_SC_ENTRY(CODE, pl_sc_static_u8, pls::OUT_U8)                                                          \
-    PL_SC_CNT_ENTRY(CODE)
+    PL_SC_CNT_ENTRY(CODE)                                                                                    \
+    PL_SC_SIM_ENTRY(CODE)
 
 #endif  // PL_SC_STATIC_H

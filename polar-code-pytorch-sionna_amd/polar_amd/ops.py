@@ -173,6 +173,36 @@ def sc_decode_count(plan, llr_logits, ref_bits, counts=None):
     return counts
 
 
+def sc_sim_count(plan, bs, no, seed, iteration, row0=0, counts=None, dump=False):
+    """pl_sc_sim_count: one Monte-Carlo iteration inside the specialised SC kernel -- information
+    bits, encoder, QPSK, AWGN and logits generated in the decoder's registers, decoded and counted
+    (System_AWGN_model.forward + my_sn/sim.py:84-100).  Accumulates [bit errors, block errors] into
+    counts (int64 [2] on the plan's device, created if None) and returns it; with dump=True returns
+    (counts, u [bs, k] fp32, logits [bs, n] fp32) as generated.  Raises PolarLibError (PL_ENOTSUP)
+    for plans without the fused entry (generic kernel, or not 64 channel slots per lane)."""
+    dev = plan.device
+    no = float(no)
+    if not no > 0.0:
+        raise ValueError(f"noise variance must be positive, got {no}")
+    bs = int(bs)
+    if counts is None:
+        counts = torch.zeros(2, dtype=torch.int64, device=dev)
+    u = llr = None
+    if dump:
+        u = torch.empty((bs, plan.k), dtype=torch.float32, device=dev)
+        llr = torch.empty((bs, plan.n), dtype=torch.float32, device=dev)
+    ws_bytes = int(_lib.lib().pl_sc_count_workspace_size(plan.handle, bs))
+    ws = torch.empty((max(ws_bytes, 4),), dtype=torch.uint8, device=dev)  # per call: stream-safe
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().pl_sc_sim_count(plan.handle, int(seed) & (2 ** 64 - 1), int(iteration) & (2 ** 64 - 1),
+                                              int(row0), bs, no, ctypes.c_void_p(counts.data_ptr()),
+                                              ctypes.c_void_p(ws.data_ptr()), ws_bytes,
+                                              ctypes.c_void_p(llr.data_ptr() if dump else None),
+                                              ctypes.c_void_p(u.data_ptr() if dump else None),
+                                              _lib.current_stream_ptr(dev)), "pl_sc_sim_count")
+    return (counts, u, llr) if dump else counts
+
+
 def count_errors(a, b, counts=None):
     """[bit errors, block errors] (int64, on the device) of two [..., k] 0/1 fp32 tensors
     (my_sn/sim.py:7-18 count_errors / count_block_errors in one pass); accumulates into counts."""

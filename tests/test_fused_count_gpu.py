@@ -6,8 +6,9 @@
     (my_sn/sim.py:7-18, via pl_count_errors) of pl_sc_decode's output against the same bits,
     exactly, for the bench code at 1, 2 and 4 dB, ragged batches, k not a multiple of 32, and
     rate-0 / rate-1 root halves (the LDS channel path);
-  * sim_ber over FusedAWGN + SC_Dec takes the fused path and its counters equal the two-kernel
-    path's for the same seed;
+  * sim_ber over FusedAWGN(sim_kernel=False) + SC_Dec takes the fused-count path and its counters
+    equal the two-kernel path's for the same seed (the producer-in-kernel path, pl_sc_sim_count,
+    is tested in tests/test_sim_kernel_gpu.py);
   * plans on the generic SC kernel report PL_ENOTSUP.
 """
 import numpy as np
@@ -94,7 +95,7 @@ def test_sim_ber_fused_equals_two_kernel_path(pa):
     fp = pa.reference_frozen_pos(k, n)
     counts = []
     for fused in (True, False):
-        model = channel.FusedAWGN(n, k, fp, pa.SC_Dec(fp, n), seed=3)
+        model = channel.FusedAWGN(n, k, fp, pa.SC_Dec(fp, n), seed=3, sim_kernel=False)
         mc = model if fused else (lambda batch_size, ebno_db, m=model: m(batch_size, ebno_db))
         _, _, cnt = sim.sim_ber(mc, [2.5, 3.0, 3.5], 8192, 3, verbose=False, device="cuda", return_counts=True)
         counts.append(cnt)

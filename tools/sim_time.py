@@ -51,6 +51,8 @@ print(f"({a.k},{a.n}) bs={a.bs} producer={a.producer}: LLR production {t_llr:.3f
       f"BLER {float(sim.count_block_errors(bits, bh)) / a.bs:.4f}", flush=True)
 if a.producer == "fused":
     counts = torch.zeros(2, dtype=torch.int64, device=dev)
-    t_fc, _ = timed(lambda: model.error_counts(a.bs, eb, counts), reps=50)
-    print(f"  sim_ber's fused path (pl_awgn_qpsk_llr_bits + pl_sc_decode_count): {t_fc:.3f} ms per iteration -> "
-          f"{a.bs / t_fc / 1e3:.1f} Mcw/s", flush=True)
+    for sk, what in ((False, "pl_awgn_qpsk_llr_bits + pl_sc_decode_count"), (True, "pl_sc_sim_count")):
+        model.sim_kernel = sk
+        t_fc, _ = timed(lambda: model.error_counts(a.bs, eb, counts), reps=50)
+        print(f"  sim_ber's fused path ({what}): {t_fc:.3f} ms per iteration -> "
+              f"{a.bs / t_fc / 1e3:.1f} Mcw/s", flush=True)
