@@ -70,6 +70,9 @@ namespace {
 #ifndef PL_SCL_RANK_MASK
 #define PL_SCL_RANK_MASK 1  // 1: 16-lane rank with a static tie mask and carry-in adds (no index DPP)
 #endif
+#ifndef PL_SCL_RANK_SUBB
+#define PL_SCL_RANK_SUBB 1  // 1: 16-lane rank as 64-bit borrow chains with DPP sources (rank16_subb)
+#endif
 #ifndef PL_SCL_WPE
 #define PL_SCL_WPE 2  // > 0: amdgpu_waves_per_eu minimum (2: <= 256 VGPRs, A/B on MI355X: 2.30 vs 3.62 ms at V=4)
 #endif
@@ -168,8 +171,51 @@ __device__ __forceinline__ int add_lane_bit(int acc, uint64_t m) {
     return r;
 }
 
+#if PL_SCL_RANK_SUBB
+// Rank of this lane's candidate in its 16-lane group (the DPP row), all 15 rotations in one
+// block.  Metrics are non-negative doubles (pm starts at 0 or llr_max > 0 and only ever adds
+// softplus values >= +0; never -0 or NaN), so their bit patterns order like the values, and the
+// stable (metric, index) comparison "v < cv, or v == cv with the lower index" is the 64-bit
+// unsigned v < cv + tie, tie = 1 exactly when the rotated source has the lower index (the same
+// static row mask as the ballot form above: group lanes >= r under row_ror:r).  Per rotation:
+// the tie mask into VCC as the borrow-in, v_subb on the low and high words with the rotated
+// candidate as the DPP source -- the final borrow is the comparison -- and one carry add into
+// the rank.  3 VALU (2 of them DPP) + 2 SALU, against 2 DPP moves + 2 fp64 compares + 1 add +
+// 3 SALU.
+#define PL_RANK_ROT(r, m)                                                                   \
+    "s_mov_b32 vcc_lo, " #m "\n\t"                                                          \
+    "s_mov_b32 vcc_hi, " #m "\n\t"                                                          \
+    "v_subb_co_u32_dpp %1, vcc, %2, %2, vcc row_ror:" #r " row_mask:0xf bank_mask:0xf\n\t" \
+    "v_subb_co_u32_dpp %1, vcc, %3, %3, vcc row_ror:" #r " row_mask:0xf bank_mask:0xf\n\t" \
+    "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n\t"
+__device__ __forceinline__ int rank16_subb(double cv) {
+    const long long b = __double_as_longlong(cv);
+    const int lo = (int)(b & 0xffffffffLL), hi = (int)(b >> 32);
+    int rk, tmp;
+    asm volatile(
+        "s_nop 1\n\t"  // the DPP sources were just written by a VALU
+        "v_mov_b32 %0, 0\n\t"
+        PL_RANK_ROT(1, 0xfffefffe) PL_RANK_ROT(2, 0xfffcfffc) PL_RANK_ROT(3, 0xfff8fff8)
+        PL_RANK_ROT(4, 0xfff0fff0) PL_RANK_ROT(5, 0xffe0ffe0) PL_RANK_ROT(6, 0xffc0ffc0)
+        PL_RANK_ROT(7, 0xff80ff80) PL_RANK_ROT(8, 0xff00ff00) PL_RANK_ROT(9, 0xfe00fe00)
+        PL_RANK_ROT(10, 0xfc00fc00) PL_RANK_ROT(11, 0xf800f800) PL_RANK_ROT(12, 0xf000f000)
+        PL_RANK_ROT(13, 0xe000e000) PL_RANK_ROT(14, 0xc000c000) PL_RANK_ROT(15, 0x80008000)
+        : "=&v"(rk), "=&v"(tmp)
+        : "v"(lo), "v"(hi)
+        : "vcc");
+    return rk;
+}
+#undef PL_RANK_ROT
+#endif
+
 template <int GW, int r>
 __device__ __forceinline__ void rank_rot(double cv, int gl, int lane, int& rk) {
+#if PL_SCL_RANK_SUBB
+    if constexpr (GW == 16 && r == 1) {
+        rk = rank16_subb(cv);
+        return;
+    }
+#endif
 #if PL_SCL_RANK_MASK
     if constexpr (GW == 16 && r < GW) {
         // row_ror:r -- group lane gl receives group lane (gl - r) mod 16, whose candidate index
