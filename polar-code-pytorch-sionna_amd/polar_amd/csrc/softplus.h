@@ -15,6 +15,29 @@
 
 namespace pl {
 
+// a * b + c as one VOP3 v_fma_f64.  Left to itself the compiler keeps the loop-invariant Horner
+// coefficient c in a VGPR, copies it into the destination and uses the two-address v_fmac_f64:
+// one extra v_mov_b64 per polynomial step (23 per penalty).  Same operation, same rounding.
+// Same-process A/B, SCL (512,1024) L=8 bs=8192 (profiles/r02zg_scl_fma_ab.txt): plain fma()
+// 1.160 ms, VGPR coefficients 1.104 ms, SGPR coefficients (s_mov pairs; 35 fewer VGPRs, more
+// SGPR spills) 1.130 ms.
+#ifndef PL_SP_FMA
+#define PL_SP_FMA 1  // 0: plain fma(), 1: VOP3 with a VGPR coefficient, 2: VOP3 with an SGPR coefficient
+#endif
+__device__ __forceinline__ double fma3(double a, double b, double c) {
+#if PL_SP_FMA == 0
+    return fma(a, b, c);
+#else
+    double d;
+#if PL_SP_FMA == 1
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+#else
+    asm("v_fma_f64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
+#endif
+    return d;
+#endif
+}
+
 __device__ __forceinline__ double pm_exp(double z) {
     constexpr double kLog2e = 1.4426950408889634;
     constexpr double kLn2Hi = 0x1.62e42fefa39efp-1, kLn2Lo = 0x1.abc9e3b39803fp-56;
@@ -23,19 +46,19 @@ __device__ __forceinline__ double pm_exp(double z) {
     r = fma(-k, kLn2Lo, r);
     // 1/i!, i = 13 .. 0
     double p = 1.6059043836821613e-10;
-    p = fma(p, r, 2.08767569878681e-09);
-    p = fma(p, r, 2.505210838544172e-08);
-    p = fma(p, r, 2.755731922398589e-07);
-    p = fma(p, r, 2.7557319223985893e-06);
-    p = fma(p, r, 2.48015873015873e-05);
-    p = fma(p, r, 0.0001984126984126984);
-    p = fma(p, r, 0.001388888888888889);
-    p = fma(p, r, 0.008333333333333333);
-    p = fma(p, r, 0.041666666666666664);
-    p = fma(p, r, 0.16666666666666666);
-    p = fma(p, r, 0.5);
-    p = fma(p, r, 1.0);
-    p = fma(p, r, 1.0);
+    p = fma3(p, r, 2.08767569878681e-09);
+    p = fma3(p, r, 2.505210838544172e-08);
+    p = fma3(p, r, 2.755731922398589e-07);
+    p = fma3(p, r, 2.7557319223985893e-06);
+    p = fma3(p, r, 2.48015873015873e-05);
+    p = fma3(p, r, 0.0001984126984126984);
+    p = fma3(p, r, 0.001388888888888889);
+    p = fma3(p, r, 0.008333333333333333);
+    p = fma3(p, r, 0.041666666666666664);
+    p = fma3(p, r, 0.16666666666666666);
+    p = fma3(p, r, 0.5);
+    p = fma3(p, r, 1.0);
+    p = fma3(p, r, 1.0);
     return ldexp(p, (int)k);
 }
 
@@ -52,17 +75,17 @@ __device__ __forceinline__ double pm_log(double y) {  // y >= 1, finite
     const double z = s * s;
     // R(z) = sum_{i>=1} 2/(2i+1) z^(i-1), i = 1 .. 12
     double R = 2.0 / 25.0;
-    R = fma(R, z, 2.0 / 23.0);
-    R = fma(R, z, 2.0 / 21.0);
-    R = fma(R, z, 2.0 / 19.0);
-    R = fma(R, z, 2.0 / 17.0);
-    R = fma(R, z, 2.0 / 15.0);
-    R = fma(R, z, 2.0 / 13.0);
-    R = fma(R, z, 2.0 / 11.0);
-    R = fma(R, z, 2.0 / 9.0);
-    R = fma(R, z, 2.0 / 7.0);
-    R = fma(R, z, 2.0 / 5.0);
-    R = fma(R, z, 2.0 / 3.0);
+    R = fma3(R, z, 2.0 / 23.0);
+    R = fma3(R, z, 2.0 / 21.0);
+    R = fma3(R, z, 2.0 / 19.0);
+    R = fma3(R, z, 2.0 / 17.0);
+    R = fma3(R, z, 2.0 / 15.0);
+    R = fma3(R, z, 2.0 / 13.0);
+    R = fma3(R, z, 2.0 / 11.0);
+    R = fma3(R, z, 2.0 / 9.0);
+    R = fma3(R, z, 2.0 / 7.0);
+    R = fma3(R, z, 2.0 / 5.0);
+    R = fma3(R, z, 2.0 / 3.0);
     const double lm = fma(s * z, R, s + s);  // log m = 2s + s z R(z)
     const double de = (double)e;
     return fma(de, kLn2Hi, fma(de, kLn2Lo, lm));
