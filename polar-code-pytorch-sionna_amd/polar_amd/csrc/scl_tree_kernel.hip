@@ -73,6 +73,9 @@ namespace {
 #ifndef PL_SCL_RANK_SUBB
 #define PL_SCL_RANK_SUBB 1  // 1: 16-lane rank as 64-bit borrow chains with DPP sources (rank16_subb)
 #endif
+#ifndef PL_SCL_FG_BITS
+#define PL_SCL_FG_BITS 1  // 1: min-sum f and g sign handling on the high words (f_ms, g_op)
+#endif
 #ifndef PL_SCL_WPE
 #define PL_SCL_WPE 2  // > 0: amdgpu_waves_per_eu minimum (2: <= 256 VGPRs, A/B on MI355X: 2.30 vs 3.62 ms at V=4)
 #endif
@@ -111,10 +114,36 @@ __host__ __device__ inline Lay make_layout(int n, int S, int L, int V) {
     return y;
 }
 
+#if PL_SCL_FG_BITS
+// v_min_f64 without the input canonicalisation fmin() adds (a v_max_f64 per operand that is not
+// known canonical); the decoder never sees NaNs (unsupported inputs)
+__device__ __forceinline__ double min_abs_nc(double a, double b) {
+    double d;
+    asm("v_min_f64 %0, |%1|, |%2|" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+}
+__device__ __forceinline__ double min_nc(double a, double b) {
+    double d;
+    asm("v_min_f64 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+}
+#endif
+
 __device__ __forceinline__ double f_ms(double x, double y, double lmax) {  // polar_scl.py:93-106
+#if PL_SCL_FG_BITS
+    // m >= +0, so sign(x) sign(y) m is m with the sign bit x31 ^ y31 (two 32-bit ops on the high
+    // words instead of a 64-bit sign test, a negation and two selects)
+    const double m = min_nc(min_abs_nc(x, y), lmax);
+    const unsigned long long mb = (unsigned long long)__double_as_longlong(m);
+    const uint32_t sx = (uint32_t)((unsigned long long)__double_as_longlong(x) >> 32);
+    const uint32_t sy = (uint32_t)((unsigned long long)__double_as_longlong(y) >> 32);
+    const uint32_t hi = (uint32_t)(mb >> 32) | ((sx ^ sy) & 0x80000000u);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | (mb & 0xffffffffull)));
+#else
     const double m = fmin(fmin(fabs(x), fabs(y)), lmax);
     const bool neg = (__double_as_longlong(x) ^ __double_as_longlong(y)) < 0;
     return neg ? -m : m;
+#endif
 }
 __device__ __forceinline__ double f_ex(double x, double y, double lmax) {  // my_sn dec.py:330-339
     const double xc = fmax(fmin(x, lmax), -lmax), yc = fmax(fmin(y, lmax), -lmax);
@@ -128,7 +157,14 @@ __device__ __forceinline__ double f_op(double x, double y, double lmax) {
     else return f_ex(x, y, lmax);
 }
 __device__ __forceinline__ double g_op(double x, double y, uint32_t bit) {  // :107-108
+#if PL_SCL_FG_BITS
+    // (1 - 2u) x + y: the bit goes straight into x's sign (a shift and a xor, which the compiler
+    // folds with the bit extraction, instead of a compare and a select)
+    const unsigned long long xb = (unsigned long long)__double_as_longlong(x);
+    return __longlong_as_double((long long)(xb ^ ((unsigned long long)(bit << 31) << 32))) + y;
+#else
     return (bit ? -x : x) + y;
+#endif
 }
 __device__ __forceinline__ uint32_t getbit(const uint32_t* w, int pos) { return (w[pos >> 5] >> (pos & 31)) & 1u; }
 
