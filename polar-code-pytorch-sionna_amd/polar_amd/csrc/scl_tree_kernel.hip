@@ -76,6 +76,13 @@ namespace {
 #ifndef PL_SCL_FG_BITS
 #define PL_SCL_FG_BITS 1  // 1: min-sum f and g sign handling on the high words (f_ms, g_op)
 #endif
+#ifndef PL_SCL_ST_UNROLL
+#define PL_SCL_ST_UNROLL 1  // 1: min-sum stored-stage node passes of 2^R / 2^(R+1) outputs unrolled, loads first
+                           // (A/B r02zk: 1.081 -> 1.050 ms)
+#endif
+#ifndef PL_SCL_ST_CH
+#define PL_SCL_ST_CH 8  // elements per lane loaded ahead in those passes
+#endif
 #ifndef PL_SCL_WPE
 #define PL_SCL_WPE 2  // > 0: amdgpu_waves_per_eu minimum (2: <= 256 VGPRs, A/B on MI355X: 2.30 vs 3.62 ms at V=4)
 #endif
@@ -500,12 +507,57 @@ __device__ void vvisit64(const St& t, int pos, bool is_g, int lane, const int* w
 // element).  When the input is virtual (s = SS + 1, V stages below the channel) each lane keeps
 // one (codeword, element) and loops over the paths, so the 2 x 2^V channel values it needs are
 // read once, not once per path (lanes idle when the node has fewer than 64 / CPW elements).
+// Stored-stage pass of node_fg with the stage size a compile-time constant (2^LS outputs per
+// path; CPW * L = 32 (codeword, path) pairs, so 2^(LS-1) elements per lane): the owner pointers,
+// operands and partial-sum words of up to 8 elements per lane are loaded before any result is
+// stored, so a pass waits for ~2 LDS round trips instead of 3 per element (the stores could alias
+// the loads as far as the compiler knows, which kept the runtime-bounded loop serial).
+template <int L, int FM, int CPW, int LS>
+__device__ __forceinline__ void node_fg_st(const St& t, int pos, bool is_g, int lane) {
+    constexpr int LL = ilog2(L), h = 1 << LS, total = CPW * L * h, IT = (total + 63) / 64;
+    constexpr int CH = IT < PL_SCL_ST_CH ? IT : PL_SCL_ST_CH;
+    const int s = LS + 1;
+    asm volatile("" : "+v"(lane));  // opaque per call: keeps the per-lane addresses from being
+                                    // hoisted out of the decoder loop (they spilled the subtree)
+#pragma unroll
+    for (int c0 = 0; c0 < IT; c0 += CH) {
+        double x[CH], y[CH];
+        uint32_t wb[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int idx = (c0 + u) * 64 + lane;
+            if (total % 64 == 0 || idx < total) {
+                const int c = idx >> (LL + LS), p = (idx >> LS) & (L - 1), j = idx & (h - 1);
+                const Cw w = t.cw(c);
+                const double* in = w.A + w.sptr[p * (t.S + 1) + s] * t.per + (1 << s) - (1 << R);
+                x[u] = in[j];
+                y[u] = in[j + h];
+                wb[u] = is_g ? w.beta[p * t.W + ((pos + j) >> 5)] : 0u;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int idx = (c0 + u) * 64 + lane;
+            if (total % 64 == 0 || idx < total) {
+                const int c = idx >> (LL + LS), p = (idx >> LS) & (L - 1), j = idx & (h - 1);
+                const Cw w = t.cw(c);
+                const double r = is_g ? g_op(x[u], y[u], (wb[u] >> ((pos + j) & 31)) & 1u)
+                                      : f_op<FM>(x[u], y[u], t.lmax);
+                w.A[p * t.per + (1 << LS) - (1 << R) + j] = r;
+            }
+        }
+    }
+}
+
 template <int L, int V, int FM, int CPW>
 __device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane) {
     constexpr int LL = ilog2(L);
     const int ls = s - 1, h = 1 << ls;
     if (PL_SCL_DIAG_SKIP_V && s > t.SS) {
     } else if (PL_SCL_DIAG_SKIP_ST && s <= t.SS) {
+    } else if (PL_SCL_ST_UNROLL && FM == 0 && s <= t.SS && ls <= R + 1) {  // exact f: spills (7.7 -> 11.2 ms)
+        if (ls == R) node_fg_st<L, FM, CPW, R>(t, pos, is_g, lane);
+        else node_fg_st<L, FM, CPW, R + 1>(t, pos, is_g, lane);
     } else if (s <= t.SS) {
         const int total = CPW * L * h;
         for (int idx = lane; idx < total; idx += 64) {
