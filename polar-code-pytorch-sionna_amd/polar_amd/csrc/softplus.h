@@ -20,9 +20,12 @@ namespace pl {
 // one extra v_mov_b64 per polynomial step (23 per penalty).  Same operation, same rounding.
 // Same-process A/B, SCL (512,1024) L=8 bs=8192 (profiles/r02zg_scl_fma_ab.txt): plain fma()
 // 1.160 ms, VGPR coefficients 1.104 ms, SGPR coefficients (s_mov pairs; 35 fewer VGPRs, more
-// SGPR spills) 1.130 ms.
+// SGPR spills) 1.130 ms.  The compiler pads each inline-asm block with hazard s_nops (15 per
+// penalty), so the default (3) issues each polynomial as one block: 1.081 vs 1.085 ms, my_sn
+// exact-f fast-SCL 7.66 vs 7.73 ms (profiles/r02zj_scl_horner_ab*.txt).
 #ifndef PL_SP_FMA
-#define PL_SP_FMA 1  // 0: plain fma(), 1: VOP3 with a VGPR coefficient, 2: VOP3 with an SGPR coefficient
+#define PL_SP_FMA 3  // 0: plain fma(), 1: VOP3 with a VGPR coefficient, 2: VOP3 with an SGPR coefficient,
+                    // 3: each polynomial as one asm block
 #endif
 __device__ __forceinline__ double fma3(double a, double b, double c) {
 #if PL_SP_FMA == 0
@@ -45,6 +48,27 @@ __device__ __forceinline__ double pm_exp(double z) {
     double r = fma(-k, kLn2Hi, z);
     r = fma(-k, kLn2Lo, r);
     // 1/i!, i = 13 .. 0
+#if PL_SP_FMA == 3
+    double p;  // the whole Horner chain in one block: no hazard padding between the steps
+    asm("v_fma_f64 %0, %2, %1, %3\n\t"
+        "v_fma_f64 %0, %0, %1, %4\n\t"
+        "v_fma_f64 %0, %0, %1, %5\n\t"
+        "v_fma_f64 %0, %0, %1, %6\n\t"
+        "v_fma_f64 %0, %0, %1, %7\n\t"
+        "v_fma_f64 %0, %0, %1, %8\n\t"
+        "v_fma_f64 %0, %0, %1, %9\n\t"
+        "v_fma_f64 %0, %0, %1, %10\n\t"
+        "v_fma_f64 %0, %0, %1, %11\n\t"
+        "v_fma_f64 %0, %0, %1, %12\n\t"
+        "v_fma_f64 %0, %0, %1, 0.5\n\t"
+        "v_fma_f64 %0, %0, %1, 1.0\n\t"
+        "v_fma_f64 %0, %0, %1, 1.0"
+        : "=&v"(p)
+        : "v"(r), "v"(1.6059043836821613e-10), "v"(2.08767569878681e-09), "v"(2.505210838544172e-08),
+          "v"(2.755731922398589e-07), "v"(2.7557319223985893e-06), "v"(2.48015873015873e-05),
+          "v"(0.0001984126984126984), "v"(0.001388888888888889), "v"(0.008333333333333333),
+          "v"(0.041666666666666664), "v"(0.16666666666666666));
+#else
     double p = 1.6059043836821613e-10;
     p = fma3(p, r, 2.08767569878681e-09);
     p = fma3(p, r, 2.505210838544172e-08);
@@ -59,6 +83,7 @@ __device__ __forceinline__ double pm_exp(double z) {
     p = fma3(p, r, 0.5);
     p = fma3(p, r, 1.0);
     p = fma3(p, r, 1.0);
+#endif
     return ldexp(p, (int)k);
 }
 
@@ -74,6 +99,24 @@ __device__ __forceinline__ double pm_log(double y) {  // y >= 1, finite
     const double s = f / (2.0 + f);
     const double z = s * s;
     // R(z) = sum_{i>=1} 2/(2i+1) z^(i-1), i = 1 .. 12
+#if PL_SP_FMA == 3
+    double R;
+    asm("v_fma_f64 %0, %2, %1, %3\n\t"
+        "v_fma_f64 %0, %0, %1, %4\n\t"
+        "v_fma_f64 %0, %0, %1, %5\n\t"
+        "v_fma_f64 %0, %0, %1, %6\n\t"
+        "v_fma_f64 %0, %0, %1, %7\n\t"
+        "v_fma_f64 %0, %0, %1, %8\n\t"
+        "v_fma_f64 %0, %0, %1, %9\n\t"
+        "v_fma_f64 %0, %0, %1, %10\n\t"
+        "v_fma_f64 %0, %0, %1, %11\n\t"
+        "v_fma_f64 %0, %0, %1, %12\n\t"
+        "v_fma_f64 %0, %0, %1, %13"
+        : "=&v"(R)
+        : "v"(z), "v"(2.0 / 25.0), "v"(2.0 / 23.0), "v"(2.0 / 21.0), "v"(2.0 / 19.0), "v"(2.0 / 17.0),
+          "v"(2.0 / 15.0), "v"(2.0 / 13.0), "v"(2.0 / 11.0), "v"(2.0 / 9.0), "v"(2.0 / 7.0), "v"(2.0 / 5.0),
+          "v"(2.0 / 3.0));
+#else
     double R = 2.0 / 25.0;
     R = fma3(R, z, 2.0 / 23.0);
     R = fma3(R, z, 2.0 / 21.0);
@@ -86,6 +129,7 @@ __device__ __forceinline__ double pm_log(double y) {  // y >= 1, finite
     R = fma3(R, z, 2.0 / 7.0);
     R = fma3(R, z, 2.0 / 5.0);
     R = fma3(R, z, 2.0 / 3.0);
+#endif
     const double lm = fma(s * z, R, s + s);  // log m = 2s + s z R(z)
     const double de = (double)e;
     return fma(de, kLn2Hi, fma(de, kLn2Lo, lm));
