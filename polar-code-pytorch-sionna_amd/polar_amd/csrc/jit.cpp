@@ -336,10 +336,20 @@ int attach_static(pl_plan* p, const uint8_t* frozen, bool allow_compile) {
         (void)hipMemcpyDtoH(&bpc, gp, sizeof(int));
     (void)hipGetLastError();
     if (bpc < 1) bpc = 1;
+    int waves = 4;  // waves per work-group (pl_sc_waves; objects built before it existed: 4)
+    if (hipModuleGetGlobal(&gp, &gsz, mod, "pl_sc_waves") == hipSuccess && gsz == sizeof(int))
+        (void)hipMemcpyDtoH(&waves, gp, sizeof(int));
+    (void)hipGetLastError();
+    if (waves != 1 && waves != 2 && waves != 4) {
+        (void)hipModuleUnload(mod);
+        set_error("specialised SC kernel: unsupported waves per work-group");
+        return PL_EINVAL;
+    }
     int dev = 0, cus = 0;
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
     p->sc_log_g = lg;
+    p->sc_waves = waves;
     p->sc_persistent = persistent;
     p->resident_blocks = bpc * cus;
     p->sc_module = mod;
@@ -358,8 +368,8 @@ void detach_static(pl_plan* p) {
 }
 
 int64_t sc_count_waves(const pl_plan* p, int64_t bs) {
-    const int64_t per_block = 4 * (64 / (1 << p->sc_log_g));
-    return ((bs + per_block - 1) / per_block) * 4;
+    const int64_t per_block = p->sc_waves * (64 / (1 << p->sc_log_g));
+    return ((bs + per_block - 1) / per_block) * p->sc_waves;
 }
 
 int launch_sc_static_count(const pl_plan* p, const float* llr, int64_t bs, const uint32_t* ref, int32_t* part,
@@ -369,7 +379,7 @@ int launch_sc_static_count(const pl_plan* p, const float* llr, int64_t bs, const
         set_error("SC decode+count: the plan's kernel is a persistent diagnostic build");
         return PL_ENOTSUP;
     }
-    const int64_t blocks = sc_count_waves(p, bs) / 4;
+    const int64_t blocks = sc_count_waves(p, bs) / p->sc_waves;
     if (blocks > 0x7fffffffLL) {
         set_error("SC decode+count: batch too large for one launch");
         return PL_EINVAL;
@@ -378,14 +388,14 @@ int launch_sc_static_count(const pl_plan* p, const float* llr, int64_t bs, const
     int k = p->k;
     const int32_t* loc = p->d_info_loc;
     void* args[] = {(void*)&llr, (void*)&bs, (void*)&part, (void*)&loc, (void*)&k, (void*)&lmax, (void*)&ref};
-    return check_hip(hipModuleLaunchKernel(p->sc_fn_cnt, (unsigned)blocks, 1, 1, 256, 1, 1, 0, st, args, nullptr),
+    return check_hip(hipModuleLaunchKernel(p->sc_fn_cnt, (unsigned)blocks, 1, 1, 64 * p->sc_waves, 1, 1, 0, st, args, nullptr),
                      "SC decode+count launch (specialised)");
 }
 
 int launch_sc_static_sim(const pl_plan* p, uint64_t seed, uint64_t iteration, int64_t row0, int64_t bs, float no,
                          int32_t* part, float* llr_dump, float* u_dump, hipStream_t st) {
     if (bs == 0) return PL_OK;
-    const int64_t blocks = sc_count_waves(p, bs) / 4;
+    const int64_t blocks = sc_count_waves(p, bs) / p->sc_waves;
     if (blocks > 0x7fffffffLL) {
         set_error("SC Monte-Carlo iteration: batch too large for one launch");
         return PL_EINVAL;
@@ -396,14 +406,14 @@ int launch_sc_static_sim(const pl_plan* p, uint64_t seed, uint64_t iteration, in
     const int32_t* loc = p->d_info_loc;
     void* args[] = {(void*)&bs,  (void*)&row0, (void*)&k0, (void*)&k1,   (void*)&it,       (void*)&no,
                     (void*)&part, (void*)&loc, (void*)&k,  (void*)&lmax, (void*)&llr_dump, (void*)&u_dump};
-    return check_hip(hipModuleLaunchKernel(p->sc_fn_sim, (unsigned)blocks, 1, 1, 256, 1, 1, 0, st, args, nullptr),
+    return check_hip(hipModuleLaunchKernel(p->sc_fn_sim, (unsigned)blocks, 1, 1, 64 * p->sc_waves, 1, 1, 0, st, args, nullptr),
                      "SC Monte-Carlo iteration launch (specialised)");
 }
 
 int launch_sc_static(const pl_plan* p, const float* llr, int64_t bs, void* out, int out_kind, hipStream_t st) {
     if (bs == 0 || p->k == 0) return PL_OK;
     const int G = 1 << p->sc_log_g;           // the layout the plan's kernel was built for
-    const int64_t per_block = 4 * (64 / G);  // pls::kWaves codeword groups of 64/G
+    const int64_t per_block = p->sc_waves * (64 / G);  // pls::kWaves codeword groups of 64/G
     int64_t blocks = (bs + per_block - 1) / per_block;
     if (p->sc_persistent && p->resident_blocks > 0 && blocks > p->resident_blocks) blocks = p->resident_blocks;
     if (blocks > 0x7fffffffLL) {
@@ -415,7 +425,7 @@ int launch_sc_static(const pl_plan* p, const float* llr, int64_t bs, void* out, 
     const int32_t* loc = p->d_info_loc;
     void* args[] = {(void*)&llr, (void*)&bs, (void*)&out, (void*)&loc, (void*)&k, (void*)&lmax};
     hipFunction_t fn = out_kind == PL_OUT_F32 ? p->sc_fn_f32 : p->sc_fn_u8;
-    return check_hip(hipModuleLaunchKernel(fn, (unsigned)blocks, 1, 1, 256, 1, 1, 0, st, args, nullptr),
+    return check_hip(hipModuleLaunchKernel(fn, (unsigned)blocks, 1, 1, 64 * p->sc_waves, 1, 1, 0, st, args, nullptr),
                      "SC decode launch (specialised)");
 }
 

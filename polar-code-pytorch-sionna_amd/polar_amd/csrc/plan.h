@@ -27,6 +27,7 @@ struct pl_plan {
     int32_t crc_deg = 0;                 // SCL CRC-aided pick: degree (0 = none) and generator
     uint32_t crc_g = 0;                  //   mask without the leading term
     int32_t sc_log_g = 0;                // specialised kernel: log2(lanes per codeword) it was built for
+    int32_t sc_waves = 4;                // waves per work-group of the specialised kernel (pl_sc_waves)
     int32_t sc_persistent = 0;           // kernel walks batches with a grid stride (grid capped)
     int32_t resident_blocks = 0;         // 256-thread blocks resident at 2 waves/SIMD on the device
 };

@@ -119,7 +119,14 @@ namespace pls {
 
 enum : int { R0 = 0, R1 = 1, REP = 2, SPC = 3, GEN = 4 };
 enum : int { OUT_F32 = 0, OUT_U8 = 1, OUT_CNT = 2, OUT_SIM = 3 };
-constexpr int kWaves = 4;  // waves per workgroup
+#ifndef PL_SC_KWAVES
+// One-wave work-groups: a wave's slot and its 8 KiB of LDS are refilled as soon as it retires,
+// instead of when the slowest of its work-group's four waves does (the waves of a SIMD finish
+// up to 1.5x apart).  Same-process A/B (profiles/r02zu_sc_ab_waves.txt, r02zv_*): (512,1024)
+// 0.0813 / 0.0807 vs 0.0817 / 0.0815 ms, (128,256) bs = 4096 0.0078 vs 0.0079 ms.
+#define PL_SC_KWAVES 1
+#endif
+constexpr int kWaves = PL_SC_KWAVES;  // waves per workgroup (the launcher reads pl_sc_waves)
 
 template <bool B, class T, class F>
 struct Cond {
@@ -1473,6 +1480,7 @@ __device__ __forceinline__ void decode_staged(const float* __restrict__ llr, int
 #define PL_SC_STATIC_KERNELS(CODE)                                                                           \
     extern "C" __device__ const int pl_sc_persistent = PL_SC_PERSIST;                                       \
     extern "C" __device__ const int pl_sc_blocks_per_cu = PL_SC_PERSIST_BPC;                                \
+    extern "C" __device__ const int pl_sc_waves = PL_SC_KWAVES;                                            \
     PL_SC_ENTRY(CODE, pl_sc_static_f32, pls::OUT_F32)                                                        \
     PL_SC_ENTRY(CODE, pl_sc_static_u8, pls::OUT_U8)                                                          \
     PL_SC_CNT_ENTRY(CODE)                                                                                    \
