@@ -83,12 +83,22 @@ namespace {
 #ifndef PL_SCL_ST_CH
 #define PL_SCL_ST_CH 8  // elements per lane loaded ahead in those passes
 #endif
+#ifndef PL_SCL_DIAG_NO_REPOINT
+#define PL_SCL_DIAG_NO_REPOINT 0  // timing diagnostic (wrong results)
+#endif
+#ifndef PL_SCL_DIAG_NO_COMBINE
+#define PL_SCL_DIAG_NO_COMBINE 0  // timing diagnostic (wrong results)
+#endif
+#ifndef PL_SCL_REPOINT_VEC
+#define PL_SCL_REPOINT_VEC 1  // 1: re-pointing in 16-byte rows, two lanes per (codeword, path) pair (n >= 128)
+#endif
 #ifndef PL_SCL_WPE
 #define PL_SCL_WPE 2  // > 0: amdgpu_waves_per_eu minimum (2: <= 256 VGPRs, A/B on MI355X: 2.30 vs 3.62 ms at V=4)
 #endif
 
 constexpr int R = PL_SCL_R;  // stage of the lane-local subtree
 constexpr int T = 1 << R;    // leaves per lane-local subtree (<= one partial-sum word)
+constexpr int SPS = 16;      // bytes per path of the stage-owner table (S + 1 <= 16), one 16-byte row
 
 __host__ __device__ constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x >> 1); }
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
@@ -110,7 +120,7 @@ __host__ __device__ inline Lay make_layout(int n, int S, int L, int V) {
     int o = 0;
     y.off_A = o; o = align16(o + (S == R ? T : L * y.per) * 8);
     y.off_beta = o; o = align16(o + L * y.W * 4);
-    y.off_sptr = o; o = align16(o + L * (S + 1));
+    y.off_sptr = o; o = align16(o + L * SPS);
     y.off_org = o; o = align16(o + L * 4);
     y.off_ps = o; o = align16(o + L * 4);
     y.off_pm = o; o = align16(o + L * 8);
@@ -311,7 +321,7 @@ __device__ double vread(const float* ch, const uint32_t* beta, int s, int pos, i
 struct Cw {
     double* A;        // [L][per] stage s (R <= s <= SS) of buffer b at A[b*per + 2^s - 2^R + j]
     uint32_t* beta;   // [L][W] partial sums by absolute position
-    uint8_t* sptr;    // [L][S+1] owner buffer of stage s
+    uint8_t* sptr;    // [L][SPS] owner buffer of stage s (s <= S)
     int* org_s;       // [L] subtree exchange: origin path
     uint32_t* ps_s;   // [L] subtree exchange: partial-sum word
     double* pm_s;     // [L] final metrics
@@ -529,7 +539,7 @@ __device__ __forceinline__ void node_fg_st(const St& t, int pos, bool is_g, int 
             if (total % 64 == 0 || idx < total) {
                 const int c = idx >> (LL + LS), p = (idx >> LS) & (L - 1), j = idx & (h - 1);
                 const Cw w = t.cw(c);
-                const double* in = w.A + w.sptr[p * (t.S + 1) + s] * t.per + (1 << s) - (1 << R);
+                const double* in = w.A + w.sptr[p * SPS + s] * t.per + (1 << s) - (1 << R);
                 x[u] = in[j];
                 y[u] = in[j + h];
                 wb[u] = is_g ? w.beta[p * t.W + ((pos + j) >> 5)] : 0u;
@@ -564,7 +574,7 @@ __device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane) {
             const int c = idx >> (LL + ls), p = (idx >> ls) & (L - 1), j = idx & (h - 1);
             const Cw w = t.cw(c);
             const uint32_t* bp = w.beta + p * t.W;
-            const double* in = w.A + w.sptr[p * (t.S + 1) + s] * t.per + (1 << s) - (1 << R);
+            const double* in = w.A + w.sptr[p * SPS + s] * t.per + (1 << s) - (1 << R);
             const double x = in[j], y = in[j + h];
             const double r = is_g ? g_op(x, y, getbit(bp, pos + j)) : f_op<FM>(x, y, t.lmax);
             w.A[p * t.per + (1 << ls) - (1 << R) + j] = r;
@@ -636,7 +646,7 @@ __device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane) {
         }
         }
     }
-    if (lane < CPW * L) t.cw(lane >> LL).sptr[(lane & (L - 1)) * (t.S + 1) + ls] = (uint8_t)(lane & (L - 1));
+    if (lane < CPW * L) t.cw(lane >> LL).sptr[(lane & (L - 1)) * SPS + ls] = (uint8_t)(lane & (L - 1));
     __syncthreads();
 }
 
@@ -998,7 +1008,7 @@ template <int V, int FM>
 __device__ __forceinline__ double upper_node_sum(const St& t, const Cw& w, int p, int s, int pos, double sg) {
     const int len = 1 << s;
     const uint32_t* bp = w.beta + p * t.W;
-    const double* in = s <= t.SS ? w.A + w.sptr[p * (t.S + 1) + s] * t.per + (1 << s) - (1 << R) : nullptr;
+    const double* in = s <= t.SS ? w.A + w.sptr[p * SPS + s] * t.per + (1 << s) - (1 << R) : nullptr;
     const int D = t.S - s;
     const int blk = len < 128 ? len : 128;
     double lvl[8];
@@ -1053,6 +1063,35 @@ __device__ __forceinline__ int node_kind(const uint32_t* __restrict__ fw, int s,
 template <int L, int CPW>
 __device__ void repoint(const St& t, int i0, int lane) {
     constexpr int LL = ilog2(L);
+#if PL_SCL_REPOINT_VEC
+    if (t.W >= 4) {
+        // two lanes per (codeword, path) pair (CPW * L = 32): one origin load each, the pair's
+        // partial-sum row in 16-byte quads (words past i0 are copied too: they belong to leaves
+        // not decided yet and are overwritten before anything reads them) and its 16-byte
+        // stage-owner row -- 6 LDS loads and 5 stores per lane instead of 22 and 22
+        asm volatile("" : "+v"(lane));  // per-call addresses (not hoisted out of the decoder loop)
+        const int cp = lane >> 1, h = lane & 1, p = cp & (L - 1);
+        const Cw cw = t.cw(cp >> LL);
+        const int o = cw.org_s[p];
+        const int nq = min(t.W >> 2, (((i0 + 31) >> 5) + 3) >> 2);
+        const uint4* src = reinterpret_cast<const uint4*>(cw.beta + o * t.W);
+        uint4 v0 = make_uint4(0u, 0u, 0u, 0u), v1 = v0, v2 = v0, v3 = v0, sp = v0;
+        if (h < nq) v0 = src[h];
+        if (h + 2 < nq) v1 = src[h + 2];
+        if (h + 4 < nq) v2 = src[h + 4];
+        if (h + 6 < nq) v3 = src[h + 6];
+        if (h == 0) sp = *reinterpret_cast<const uint4*>(cw.sptr + o * SPS);
+        __syncthreads();
+        uint4* dst = reinterpret_cast<uint4*>(cw.beta + p * t.W);
+        if (h < nq) dst[h] = v0;
+        if (h + 2 < nq) dst[h + 2] = v1;
+        if (h + 4 < nq) dst[h + 4] = v2;
+        if (h + 6 < nq) dst[h + 6] = v3;
+        if (h == 0) *reinterpret_cast<uint4*>(cw.sptr + p * SPS) = sp;
+        __syncthreads();
+        return;
+    }
+#endif
     const int W = t.W, w_lim = (i0 + 31) >> 5;
     // CPW * L = 32 (codeword, path) pairs per wave, <= 32 words each (n <= 1024)
     constexpr int RB = 32 * 32 / 64;
@@ -1068,14 +1107,14 @@ __device__ void repoint(const St& t, int i0, int lane) {
     }
     constexpr int RS = (32 * 11 + 63) / 64;
     uint8_t vs[RS];
-    const int S1 = t.S + 1;
+    const int S1 = t.S + 1;  // entries per row (rows are SPS bytes apart)
 #pragma unroll
     for (int r = 0; r < RS; ++r) {
         const int idx = r * 64 + lane;
         if (idx < 32 * S1) {
             const int cp = idx / S1, e = idx - cp * S1;
             const Cw cw = t.cw(cp >> LL);
-            vs[r] = cw.sptr[cw.org_s[cp & (L - 1)] * S1 + e];
+            vs[r] = cw.sptr[cw.org_s[cp & (L - 1)] * SPS + e];
         }
     }
     __syncthreads();
@@ -1090,7 +1129,7 @@ __device__ void repoint(const St& t, int i0, int lane) {
         const int idx = r * 64 + lane;
         if (idx < 32 * S1) {
             const int cp = idx / S1, e = idx - cp * S1;
-            t.cw(cp >> LL).sptr[(cp & (L - 1)) * S1 + e] = vs[r];
+            t.cw(cp >> LL).sptr[(cp & (L - 1)) * SPS + e] = vs[r];
         }
     }
     __syncthreads();
@@ -1157,9 +1196,9 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
     const Cw mine = t.cw(my_c);
 
     for (int i = lane; i < CPW * L * W; i += 64) t.cw(i >> (LL + LW)).beta[i & (L * W - 1)] = 0u;
-    for (int i = lane; i < CPW * L * (S + 1); i += 64) {
-        const int c = i / (L * (S + 1)), e = i - c * (L * (S + 1));
-        t.cw(c).sptr[e] = (uint8_t)(e / (S + 1));
+    for (int i = lane; i < CPW * L * SPS; i += 64) {
+        const int c = i / (L * SPS), e = i - c * (L * SPS);
+        t.cw(c).sptr[e] = (uint8_t)(e / SPS);
     }
     if (S == R)  // the whole tree is one lane-local subtree: its input is the channel, as fp64
         for (int i = lane; i < CPW * T; i += 64) {
@@ -1207,7 +1246,7 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
             // subtree's partial sums: partial-sum words before i0 and stage owners R..SS
             if (gl < L) mine.org_s[gl] = org;
             __syncthreads();
-            repoint<L, CPW>(t, i0, lane);
+            if (!PL_SCL_DIAG_NO_REPOINT) repoint<L, CPW>(t, i0, lane);
             const int w_i = i0 >> 5, off = i0 & 31;
             if (gl < L) {
                 uint32_t* bw = mine.beta + gl * W + w_i;
@@ -1219,7 +1258,8 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
         // nodes above R that end here
         const int nxt = q << R;
         const int top2 = nxt < n ? __builtin_ctz(nxt) : S;
-        for (int s = R + 1; s <= top2; ++s) combine_upper<L, CPW>(t, s, nxt - (1 << s), lane);
+        if (!PL_SCL_DIAG_NO_COMBINE)
+            for (int s = R + 1; s <= top2; ++s) combine_upper<L, CPW>(t, s, nxt - (1 << s), lane);
     }
     if (gl < L) mine.pm_s[gl] = pm;
 
