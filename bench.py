@@ -255,10 +255,12 @@ def main():
         step()
     e1.record(stream)
     torch.cuda.synchronize(dev)
+    # this rank's time for its K steps (taken before the closing barrier, so the barrier's own
+    # latency is not part of a rank's time; the max over ranks below is the job's time)
+    wall = time.perf_counter() - t0
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    wall = time.perf_counter() - t0
     kern_ms = e0.elapsed_time(e1) / a.steps
 
     cdev = dev if os.environ.get("PL_BENCH_BACKEND", "nccl") == "nccl" else torch.device("cpu")  # gloo: host
