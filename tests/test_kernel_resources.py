@@ -1,0 +1,80 @@
+"""Register and scratch budgets of the two bench kernels, read from hipcc's gfx950 assembly (CPU).
+
+The measured throughput of both decoders rests on occupancy facts that a source change can break
+silently (DESIGN.md sections 3.1 and 3.2):
+  * the specialised SC kernel of the BASELINE code (512,1024) runs 4 waves per SIMD: <= 128 VGPRs,
+    no VGPR spills, no scratch;
+  * the SCL subtree kernel at L = 8 (min-sum, no fast-SCL: the bench kernel) runs 2 waves per SIMD
+    with no VGPR spills and no scratch (each round-2 change was checked against this; spills cost
+    5-20 % whenever they appeared).
+The sources are compiled exactly as build() / the code-object cache compile them, to assembly only.
+"""
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+from polar_amd import build as _build
+
+HIPCC = os.path.join(_build.ROCM, "bin", "hipcc")
+pytestmark = pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+
+
+def _kernel_meta(asm, name_pred):
+    """{kernel name: {field: int}} from the amdhsa metadata of an assembly file."""
+    out = {}
+    for block in asm.split("  - .agpr_count")[1:]:
+        m = re.search(r"\.name:\s+(\S+)", block)
+        if not m or not name_pred(m.group(1)):
+            continue
+        fields = {}
+        for key in ("vgpr_count", "vgpr_spill_count", "sgpr_spill_count", "private_segment_fixed_size"):
+            f = re.search(r"\." + key + r":\s+(\d+)", block)
+            fields[key] = int(f.group(1)) if f else None
+        out[m.group(1)] = fields
+    return out
+
+
+def _compile_asm(src_path, extra, workdir):
+    out = os.path.join(workdir, "k.s")
+    cmd = [HIPCC, f"--offload-arch={_build.ARCH}", "-O3", "-std=c++17", "-ffp-contract=off", *extra,
+           "--cuda-device-only", "-S", src_path, "-o", out]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return open(out).read()
+
+
+def test_scl_bench_kernel_has_no_spills_or_scratch():
+    src = os.path.join(_build.CSRC, "scl_tree_kernel.hip")
+    with tempfile.TemporaryDirectory() as td:
+        asm = _compile_asm(src, ["-DPL_SCL_TREE_L=8"], td)
+    # scl_tree_kernel<L = 8, V = 4, f_mode = 0 (min-sum), FAST = false>: the kernel bench.py --decoder scl runs
+    meta = _kernel_meta(asm, lambda n: "scl_tree_kernelILi8ELi4ELi0ELb0E" in n)
+    assert len(meta) == 1, list(meta)
+    (m,) = meta.values()
+    assert m["vgpr_spill_count"] == 0, m
+    assert m["private_segment_fixed_size"] == 0, m
+    assert m["vgpr_count"] <= 256, m  # amdgpu_waves_per_eu(2)
+
+
+def test_sc_bench_kernel_fits_four_waves_per_simd():
+    import polar_amd
+    from polar_amd import _lib
+    fp = polar_amd.reference_frozen_pos(512, 1024).numpy()
+    src, _ = _lib.sc_source(1024, polar_amd.frozen_mask(fp, 1024), _lib.PL_F_MINSUM)
+    flags, _ = _lib._source_header(src)
+    extra = [f for f in flags if f not in ("--genco", "--no-gpu-bundle-output", "-O3", "-std=c++17",
+                                           "-ffp-contract=off") and not f.startswith("--offload-arch")]
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "sc.hip")
+        with open(path, "w") as f:
+            f.write(src)
+        asm = _compile_asm(path, extra, td)
+    meta = _kernel_meta(asm, lambda n: n in ("pl_sc_static_f32", "pl_sc_static_sim"))
+    assert set(meta) == {"pl_sc_static_f32", "pl_sc_static_sim"}, list(meta)
+    for name, m in meta.items():
+        assert m["vgpr_count"] <= 128, (name, m)  # 4 waves per SIMD (512 VGPRs per lane)
+        assert m["vgpr_spill_count"] == 0, (name, m)
+        assert m["private_segment_fixed_size"] == 0, (name, m)
