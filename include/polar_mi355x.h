@@ -158,6 +158,10 @@ int pl_rate_recover(const float* llr, int64_t bs, int32_t e, const int32_t* src_
  *                  (x_run enc.py:30-43), Gray QPSK (mapping.py:136-149), AWGN of variance no
  *                  (awgn.py:19-29), logits log P(b=1)/P(b=0) (mapping.py:225-241).
  *                  u_out (nullable): [bs, k] fp32 0/1; llr_out: [bs, n] fp32.  no > 0.
+ *                  Stream keys: row0 + row is the 64-bit counter row (words 0-1); iteration is
+ *                  one 32-bit counter word, so 0 <= iteration < 2^32 (PL_EINVAL otherwise).
+ *                  polar_amd.channel.FusedAWGN keys a draw by (SNR point, iteration) with the
+ *                  point in the row's high word: row0 + (point << 32), iteration.
  * pl_count_errors: count_errors + count_block_errors (my_sn/sim.py:7-18) of two [rows, k] fp32 0/1
  *                  tensors: counts[0] += differing elements, counts[1] += rows with a difference
  *                  (int64 device counters, accumulated).
@@ -179,7 +183,8 @@ int pl_rate_recover(const float* llr, int64_t bs, int32_t e, const int32_t* src_
  *                  LLR or bit row is written unless llr_dump ([bs, n] fp32 logits) / u_dump ([bs, k]
  *                  fp32 information bits) are given (nullable; for tests).  workspace as
  *                  pl_sc_decode_count.  PL_ENOTSUP unless the plan's specialised kernel has 64
- *                  channel slots per lane (min-sum n = 64 ... 1024; pl_plan_kernel: 1). */
+ *                  channel slots per lane (min-sum n = 64 ... 1024; pl_plan_kernel: 1).
+ *                  0 <= iteration < 2^32, as pl_awgn_qpsk_llr. */
 int pl_awgn_qpsk_llr(const pl_plan* plan, uint64_t seed, uint64_t iteration, int64_t row0, int64_t bs, float no,
                      float* u_out, float* llr_out, void* hip_stream);
 int pl_awgn_qpsk_llr_bits(const pl_plan* plan, uint64_t seed, uint64_t iteration, int64_t row0, int64_t bs,

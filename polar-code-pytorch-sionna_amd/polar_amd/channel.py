@@ -202,10 +202,16 @@ class FusedAWGN(nn.Module):
     """System_AWGN_model (awgn_model.py:17-44) with the whole producer -- bits, polar encoder, QPSK
     mapper, AWGN, demapper -- as one HIP kernel per call (pl_awgn_qpsk_llr).
 
-    Same interface: forward(batch_size, ebno_db) -> (bits, bits_hat) (or (codewords=None, bits_hat)
+    Same interface: forward(batch_size, ebno_db) -> (bits, bits_hat) (or (codewords, bits_hat)
     with cw_estimates), llrs(batch_size, ebno_db) -> (bits, None, logits).  Randomness is Philox
-    keyed by `seed`; every call draws a fresh iteration of the stream (`iteration` counts calls),
-    and `row0` offsets the rows (a rank's shard of a multi-GPU batch)."""
+    keyed by `seed`.  A draw is keyed by (SNR point, iteration): forward / llrs / error_counts take
+    stream=(point, iteration) (sim_ber passes its loop indices, so a speculatively launched
+    iteration never shifts another point's codewords); without it every call draws the next
+    iteration of point 0 (`iteration` counts those calls).  Stream row r of a draw is codeword
+    row0 + r; the point lives in the row's high 32 bits (counter word 1), so row0 + batch_size
+    must stay below 2^32.  `row0` offsets the rows (a rank's shard of a multi-GPU batch)."""
+
+    keyed_streams = True  # sim_ber: draws depend on (point, iteration), not on call order
 
     def __init__(self, n, k, frozen_pos, decoder, device=None, seed=42, row0=0, cw_estimates=False,
                  sim_kernel=True):
@@ -219,6 +225,8 @@ class FusedAWGN(nn.Module):
         self.decoder = decoder
         self.cw_estimates = cw_estimates
         self.seed, self.row0, self.iteration = int(seed), int(row0), 0
+        if not 0 <= self.row0 < 2 ** 32:
+            raise ValueError(f"row0 must be in [0, 2^32), got {row0}")
         self._mask = frozen_mask(frozen_pos, self.n)
         assert self.n - int(self._mask.sum()) == self.k, "k must equal n - len(frozen_pos)"
         self.device = tc.device(device) if device is not None else tc.device("cuda", tc.cuda.current_device())
@@ -228,23 +236,38 @@ class FusedAWGN(nn.Module):
         from . import _lib
         return _lib.Plan(self.n, self._mask, 1, flags=_lib.PL_PLAN_GENERIC, device=dev)
 
-    def llrs(self, batch_size, ebno_db):
+    def _draw(self, batch_size, stream):
+        """(iteration, first stream row) of a draw of batch_size codewords."""
+        if stream is None:
+            point, it = 0, self.iteration
+            self.iteration += 1
+        else:
+            point, it = int(stream[0]), int(stream[1])
+        if not 0 <= it < 2 ** 32:
+            raise ValueError(f"Monte-Carlo iteration must be in [0, 2^32), got {it}")
+        if not 0 <= point < 2 ** 31:
+            raise ValueError(f"SNR point index must be in [0, 2^31), got {point}")
+        if self.row0 + int(batch_size) > 2 ** 32:
+            raise ValueError("row0 + batch_size must not exceed 2^32 (the point index is the row's high word)")
+        return it, self.row0 + (point << 32)
+
+    def llrs(self, batch_size, ebno_db, stream=None):
         from . import ops
         no = float(ebnodb2no(float(ebno_db), self.n_bits_per_sym, self.coderate))
-        it = self.iteration
-        self.iteration += 1
+        it, row0 = self._draw(batch_size, stream)
         bits, llr = ops.awgn_qpsk_llr(self._plans.get(self.device, self._make_plan), int(batch_size), no,
-                                      self.seed, it, self.row0)
+                                      self.seed, it, row0)
         return bits, None, llr
 
-    def forward(self, batch_size, ebno_db):
-        bits, _, llr = self.llrs(batch_size, ebno_db)
+    def forward(self, batch_size, ebno_db, stream=None):
+        bits, _, llr = self.llrs(batch_size, ebno_db, stream)
         bits_hat = self.decoder(llr)
         if self.cw_estimates:
-            return None, bits_hat
+            from . import ops
+            return ops.polar_encode(self._plans.get(self.device, self._make_plan), bits), bits_hat
         return bits, bits_hat
 
-    def error_counts(self, batch_size, ebno_db, counts=None):
+    def error_counts(self, batch_size, ebno_db, counts=None, stream=None):
         """One Monte-Carlo iteration straight to the harness's counters: [bit errors, block errors]
         (int64 [2] on the device, accumulated into counts) of decoding a fresh batch -- what
         count_errors / count_block_errors (my_sn/sim.py:7-18) give on forward()'s output.
@@ -265,17 +288,16 @@ class FusedAWGN(nn.Module):
         if plan.kernel()[0] != "specialized":
             return None
         no = float(ebnodb2no(float(ebno_db), self.n_bits_per_sym, self.coderate))
-        it = self.iteration
-        self.iteration += 1
+        it, row0 = self._draw(batch_size, stream)
         if self.sim_kernel:
             try:
-                return ops.sc_sim_count(plan, int(batch_size), no, self.seed, it, self.row0, counts)
+                return ops.sc_sim_count(plan, int(batch_size), no, self.seed, it, row0, counts)
             except _lib.PolarLibError as e:
                 if e.code != _lib.PL_ENOTSUP:
                     raise
                 self.sim_kernel = False  # this plan's kernel has no fused entry: the two-kernel path
         ubits, llr = ops.awgn_qpsk_llr_bits(self._plans.get(self.device, self._make_plan), int(batch_size), no,
-                                            self.seed, it, self.row0)
+                                            self.seed, it, row0)
         return ops.sc_decode_count(plan, llr, ubits, counts)
 
 

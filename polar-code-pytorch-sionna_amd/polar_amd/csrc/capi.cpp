@@ -276,8 +276,8 @@ int pl_sc_decode_count(const pl_plan* p, const float* llr, int64_t bs, const uin
 
 int pl_sc_sim_count(const pl_plan* p, uint64_t seed, uint64_t iteration, int64_t row0, int64_t bs, float no,
                     int64_t* counts, void* ws, size_t ws_bytes, float* llr_dump, float* u_dump, void* stream) {
-    if (!p || bs < 0 || row0 < 0 || !counts || !(no > 0.0f)) {
-        pl::set_error("pl_sc_sim_count: bad arguments (no must be > 0)");
+    if (!p || bs < 0 || row0 < 0 || !counts || !(no > 0.0f) || (iteration >> 32) != 0) {
+        pl::set_error("pl_sc_sim_count: bad arguments (no must be > 0, iteration < 2^32)");
         return PL_EINVAL;
     }
     if (p->list_size != 1) {

@@ -360,8 +360,8 @@ extern "C" {
 
 static int awgn_launch(const pl_plan* p, uint64_t seed, uint64_t iteration, int64_t row0, int64_t bs, float no,
                        float* u_out, uint32_t* ubits_out, float* llr_out, void* stream, const char* what) {
-    if (!p || bs < 0 || row0 < 0 || (bs > 0 && !llr_out) || !(no > 0.0f)) {
-        pl::set_error(std::string(what) + ": bad arguments (no must be > 0)");
+    if (!p || bs < 0 || row0 < 0 || (bs > 0 && !llr_out) || !(no > 0.0f) || (iteration >> 32) != 0) {
+        pl::set_error(std::string(what) + ": bad arguments (no must be > 0, iteration < 2^32)");
         return PL_EINVAL;
     }
     if (int r = pl::check_device(p, static_cast<hipStream_t>(stream), what)) return r;

@@ -16,6 +16,20 @@ def _require_cuda(t, name):
                            f"{getattr(t, 'device', type(t))}); the MI355X decoder has no CPU path")
 
 
+def _counts(counts, device):
+    """The int64 device counters a counting kernel accumulates into with 64-bit atomics: created
+    if None, else checked (contiguous int64 with >= 2 elements on `device`), so a host, narrower
+    or foreign-device tensor never reaches the kernel as a raw pointer."""
+    if counts is None:
+        return torch.zeros(2, dtype=torch.int64, device=device)
+    if not isinstance(counts, torch.Tensor) or counts.dtype != torch.int64 or not counts.is_contiguous() \
+            or counts.numel() < 2 or counts.device != torch.device(device):
+        raise ValueError(f"counts must be a contiguous int64 tensor of >= 2 elements on {device}, got "
+                         f"{getattr(counts, 'dtype', type(counts))} {tuple(getattr(counts, 'shape', ()))} on "
+                         f"{getattr(counts, 'device', None)}")
+    return counts
+
+
 def _out_kind(dtype):
     if dtype == torch.float32:
         return _lib.PL_OUT_F32
@@ -104,6 +118,8 @@ def awgn_qpsk_llr(plan, bs, no, seed, iteration, row0=0, with_bits=True):
     no = float(no)
     if not no > 0.0:
         raise ValueError(f"noise variance must be positive, got {no}")
+    if not 0 <= int(iteration) < 2 ** 32:
+        raise ValueError(f"iteration must be in [0, 2^32) (the Philox counter word), got {iteration}")
     llr = torch.empty((bs, plan.n), dtype=torch.float32, device=dev)
     u = torch.empty((bs, plan.k), dtype=torch.float32, device=dev) if with_bits else None
     with torch.cuda.device(dev):
@@ -123,6 +139,8 @@ def awgn_qpsk_llr_bits(plan, bs, no, seed, iteration, row0=0):
     no = float(no)
     if not no > 0.0:
         raise ValueError(f"noise variance must be positive, got {no}")
+    if not 0 <= int(iteration) < 2 ** 32:
+        raise ValueError(f"iteration must be in [0, 2^32) (the Philox counter word), got {iteration}")
     llr = torch.empty((bs, plan.n), dtype=torch.float32, device=dev)
     ubits = torch.empty((bs, (plan.k + 31) // 32), dtype=torch.int32, device=dev)
     with torch.cuda.device(dev):
@@ -161,8 +179,7 @@ def sc_decode_count(plan, llr_logits, ref_bits, counts=None):
     if ref_bits.shape != (bs, nq) or ref_bits.dtype != torch.int32 or ref_bits.device != x.device:
         raise ValueError(f"ref_bits must be int32 [{bs}, {nq}] on the input's device")
     ref = ref_bits.contiguous()
-    if counts is None:
-        counts = torch.zeros(2, dtype=torch.int64, device=x.device)
+    counts = _counts(counts, x.device)
     ws_bytes = int(_lib.lib().pl_sc_count_workspace_size(plan.handle, bs))
     ws = torch.empty((max(ws_bytes, 4),), dtype=torch.uint8, device=x.device)  # per call: stream-safe
     with torch.cuda.device(x.device):
@@ -185,8 +202,9 @@ def sc_sim_count(plan, bs, no, seed, iteration, row0=0, counts=None, dump=False)
     if not no > 0.0:
         raise ValueError(f"noise variance must be positive, got {no}")
     bs = int(bs)
-    if counts is None:
-        counts = torch.zeros(2, dtype=torch.int64, device=dev)
+    if not 0 <= int(iteration) < 2 ** 32:
+        raise ValueError(f"iteration must be in [0, 2^32) (the Philox counter word), got {iteration}")
+    counts = _counts(counts, dev)
     u = llr = None
     if dump:
         u = torch.empty((bs, plan.k), dtype=torch.float32, device=dev)
@@ -214,8 +232,7 @@ def count_errors(a, b, counts=None):
     x = a.to(torch.float32).contiguous()
     y = b.to(torch.float32).contiguous()
     rows = x.numel() // k if k else 0
-    if counts is None:
-        counts = torch.zeros(2, dtype=torch.int64, device=a.device)
+    counts = _counts(counts, a.device)
     with torch.cuda.device(a.device):
         _lib.check(_lib.lib().pl_count_errors(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(y.data_ptr()), rows, k,
                                               ctypes.c_void_p(counts.data_ptr()), _lib.current_stream_ptr(a.device)),

@@ -61,6 +61,40 @@ def test_two_rank_counters_allreduce(tmp_path):
     assert (r[0]["cnt"][:, 1] > 0).all()
 
 
+def _keyed_worker(rank, world, port, out_dir):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "polar-code-pytorch-sionna_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from polar_amd import sim
+    from test_sim_window import KeyedModel
+    bs = 12
+    m = KeyedModel(row0=rank * bs, rows_total=world * bs)
+    _, _, cnt = sim.sim_ber(m, np.array([0.0, 2.0, 4.0, 7.0]), bs, max_mc_iter=9, target_block_errs=30,
+                            verbose=False, process_group=dist.group.WORLD, return_counts=True)
+    dist.destroy_process_group()
+    np.savez(os.path.join(out_dir, f"k{rank}.npz"), cnt=cnt.numpy())
+
+
+def test_two_rank_windowed_shards_equal_one_rank(tmp_path):
+    """Windowed sim_ber over 2 gloo ranks, each drawing its rows of the keyed stream: the global
+    counters equal one rank simulating all rows (same codewords, same stop decisions)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from polar_amd import sim
+    from test_sim_window import KeyedModel
+    world = 2
+    mp.spawn(_keyed_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    r = [np.load(tmp_path / f"k{i}.npz")["cnt"] for i in range(world)]
+    np.testing.assert_array_equal(r[0], r[1])
+    _, _, one = sim.sim_ber(KeyedModel(), np.array([0.0, 2.0, 4.0, 7.0]), world * 12, max_mc_iter=9,
+                            target_block_errs=30, verbose=False, return_counts=True)
+    np.testing.assert_array_equal(r[0], one.numpy())
+    assert (r[0][:, 3] % (world * 12) == 0).all() and r[0][0, 1] >= 30
+
+
 def test_cli_parses_reference_flags():
     import sys
     sys.path.insert(0, os.path.join(ROOT, "polar-code-pytorch-sionna_amd"))

@@ -1,0 +1,114 @@
+"""configs[4] on the one GPU of the box: the sharded Monte-Carlo BLER sweep (my_sn/sim.py:79-133,
+x_run_sn_polar/main.py:55-59) through the fused path (FusedAWGN + SC_Dec -> pl_sc_sim_count) with
+sim_ber's windowed loop.
+
+  * 2 ranks sharing cuda:0 over gloo (one process per rank, as torchrun launches them), each
+    drawing stream rows [r * 65536, (r + 1) * 65536) at (512,1024), Eb/N0 0 ... 4 dB, with a
+    block-error target that stops points mid-window: the summed counters are EXACTLY those of
+    one rank simulating all 131072 rows (row0 0) -- same codewords, same stop decisions;
+  * the windowed loop equals the one-iteration loop (max_window=1) for the fused SC path and for
+    an SCL decoder behind FusedAWGN (forward() + pl_count_errors);
+  * the (512,1024) BLER matches the reference's measured table (x_run SC,
+    bs = 8192) within 5 sigma of the two binomial samples (+ one reference count).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EBNO = np.arange(0.0, 4.01, 0.5)  # configs[4]: Eb/N0 0-4 dB
+BS = 65536
+TARGET = 200_000  # block errors: points stop after 2 or 3 of max_mc_iter=4 iterations
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _sweep(rank, bs, process_group=None, max_window=None):
+    import polar_amd
+    from polar_amd import channel, sim
+    k, n = 512, 1024
+    fp = polar_amd.reference_frozen_pos(k, n)
+    dec = polar_amd.SC_Dec(fp, n)
+    model = channel.FusedAWGN(n, k, fp, dec, device=torch.device("cuda", 0), seed=42, row0=rank * bs)
+    _, _, cnt = sim.sim_ber(model, EBNO, bs, max_mc_iter=4, target_block_errs=TARGET, verbose=False,
+                            device="cpu", process_group=process_group, return_counts=True, max_window=max_window)
+    assert model.sim_kernel, "the sweep must run the fused pl_sc_sim_count path"
+    return cnt.numpy()
+
+
+def _worker(rank, world, port, out_dir):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "polar-code-pytorch-sionna_amd"))
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cnt = _sweep(rank, BS, process_group=dist.group.WORLD)
+    finally:
+        dist.destroy_process_group()
+    np.save(os.path.join(out_dir, f"r{rank}.npy"), cnt)
+
+
+def test_two_ranks_one_gpu_equal_one_rank(tmp_path):
+    import torch.multiprocessing as mp
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    r = [np.load(tmp_path / f"r{i}.npy") for i in range(world)]
+    np.testing.assert_array_equal(r[0], r[1])
+    one = _sweep(0, world * BS)
+    np.testing.assert_array_equal(r[0], one)
+    blocks = one[:, 3] // (world * BS)
+    assert set(blocks.tolist()) >= {2, 3}, blocks  # points stopped at different iterations
+    assert (one[:, 1] >= TARGET).all() or (blocks == 4).any()
+
+
+def test_window_equals_sequential_fused():
+    a = _sweep(0, 16384)
+    b = _sweep(0, 16384, max_window=1)
+    np.testing.assert_array_equal(a, b)
+
+
+def test_window_equals_sequential_scl_forward():
+    import polar_amd
+    from polar_amd import channel, sim
+    k, n = 128, 256
+    fp = polar_amd.reference_frozen_pos(k, n)
+    res = []
+    for w in (None, 1):
+        model = channel.FusedAWGN(n, k, fp, polar_amd.SCL_Dec(fp, n, 4, device="cuda"), seed=5)
+        assert model.error_counts(16, 1.0) is None  # SCL: forward() + pl_count_errors
+        _, _, c = sim.sim_ber(model, np.array([1.0, 2.0, 3.0]), 512, max_mc_iter=7, target_block_errs=300,
+                              verbose=False, device="cuda", return_counts=True, max_window=w)
+        res.append(c.numpy())
+    np.testing.assert_array_equal(res[0], res[1])
+
+
+REF_BLER_1024 = {2.0: .9999, 2.5: .9954, 3.0: .9735, 3.5: .8981, 4.0: .7612, 4.5: .5254}
+
+
+def test_bler_matches_reference_table_512_1024():
+    import polar_amd
+    from polar_amd import channel, sim
+    k, n = 512, 1024
+    fp = polar_amd.reference_frozen_pos(k, n)
+    model = channel.FusedAWGN(n, k, fp, polar_amd.SC_Dec(fp, n), seed=1234)
+    pts = np.array(sorted(REF_BLER_1024))
+    _, bler, c = sim.sim_ber(model, pts, BS, max_mc_iter=2, verbose=False, device="cuda", return_counts=True)
+    n_ref = 8192
+    for i, e in enumerate(pts):
+        p_ref, p = REF_BLER_1024[e], float(bler[i])
+        n_ours = int(c[i, 3])
+        assert n_ours == 2 * BS
+        q = (p_ref * n_ref + p * n_ours) / (n_ref + n_ours)
+        sigma = np.sqrt(q * (1 - q) * (1 / n_ref + 1 / n_ours))
+        assert abs(p - p_ref) <= 5 * sigma + 1 / n_ref, (e, p, p_ref, sigma)
