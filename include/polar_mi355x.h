@@ -56,6 +56,9 @@ extern "C" {
 #define PL_PLAN_FAST_SCL 4u   /* pl_plan_create flag (SCL): fast-SCL rate-0 / repetition pruning of
                                  my_sn/fec/polar/dec.py:367-376 (use with f_mode PL_F_EXACT for
                                  my_sn SCL_Dec semantics) */
+#define PL_PLAN_JIT 8u        /* pl_plan_create flag (SC): compile a specialised kernel missing from
+                                 the caches in this process (hiprtc, seconds); without it a cache
+                                 miss runs the generic kernel */
 
 #define PL_KERNEL_GENERIC 0     /* pl_plan_kernel kinds */
 #define PL_KERNEL_SPECIALIZED 1
@@ -72,10 +75,14 @@ typedef struct pl_plan pl_plan;
  * list_size:   1 for SC plans; a power of two <= 32 for SCL plans.
  * f_mode:      PL_F_MINSUM or PL_F_EXACT.  llr_max: clipping bound (reference: 30; at most 700
  *              for list_size > 1, where log(1 + exp(llr_max)) must stay finite).
- * flags:       0, or PL_PLAN_GENERIC / PL_PLAN_CACHE_ONLY.  By default an SC plan (list_size 1)
- *              runs a kernel specialised to its frozen set: compiled with hiprtc at plan creation
- *              (seconds) unless a cached code object exists ($PL_KERNEL_CACHE, <library dir>/kcache,
- *              ~/.cache/polar_mi355x); PL_SC_SPECIALIZE=0 in the environment disables this.
+ * flags:       0, or PL_PLAN_GENERIC / PL_PLAN_CACHE_ONLY / PL_PLAN_JIT (/ PL_PLAN_FAST_SCL).
+ *              An SC plan (list_size 1) runs a kernel specialised to its frozen set when a code
+ *              object for it is cached ($PL_KERNEL_CACHE, <library dir>/kcache,
+ *              ~/.cache/polar_mi355x; pl_sc_source + hipcc --genco, or pl_sc_specialize, put it
+ *              there), otherwise the generic kernel (also exact).  PL_PLAN_JIT compiles a missing
+ *              one in-process with hiprtc at plan creation (seconds; not in a process whose HIP
+ *              runtime came with another ROCm's amd_comgr, e.g. torch's).  PL_SC_SPECIALIZE=0 in
+ *              the environment selects the generic kernel.
  * n must be a power of two, 2 <= n <= 2048.  List plans: list_size <= 32 for n <= 1024,
  * list_size <= 16 at n = 2048 (the list state of one codeword must fit one CU's LDS); larger ones
  * are rejected here with PL_ENOTSUP. */

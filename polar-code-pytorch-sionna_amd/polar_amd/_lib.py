@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(_HERE, "libpolar_mi355x.so")
 PL_OK, PL_EINVAL, PL_EHIP, PL_ENOTSUP = 0, -1, -2, -3
 PL_F_MINSUM, PL_F_EXACT = 0, 1
 PL_OUT_F32, PL_OUT_U8 = 0, 1
-PL_PLAN_GENERIC, PL_PLAN_CACHE_ONLY, PL_PLAN_FAST_SCL = 1, 2, 4
+PL_PLAN_GENERIC, PL_PLAN_CACHE_ONLY, PL_PLAN_FAST_SCL, PL_PLAN_JIT = 1, 2, 4, 8
 PL_KERNEL_GENERIC, PL_KERNEL_SPECIALIZED, PL_KERNEL_SCL_SUBTREE = 0, 1, 2
 
 _lock = threading.Lock()
@@ -69,6 +69,18 @@ def _declare(L):
               L.pl_awgn_qpsk_llr_bits, L.pl_sc_decode_count, L.pl_sc_sim_count):
         f.restype = ctypes.c_int
     return L
+
+
+def use_dev_library():
+    """Development tools only (tools/): load libpolar_mi355x_dev.so (python -m polar_amd.build
+    --dev), the build with the A/B hooks (PL_SC_DEFINES, PL_SC_SOURCE, PL_SC_LOG_G,
+    PL_SCL_VIRTUAL, PL_SCL_TREE_FAST and the diagnostic macros), instead of the release library.
+    Must be called before the first library call of the process."""
+    global LIB_PATH
+    dev = os.path.join(_HERE, "libpolar_mi355x_dev.so")
+    if _lib is not None and LIB_PATH != dev:
+        raise PolarLibError("use_dev_library(): the release library is already loaded in this process")
+    LIB_PATH = dev
 
 
 def lib():

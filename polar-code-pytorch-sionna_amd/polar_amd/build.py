@@ -54,21 +54,31 @@ def _embed_static_source():
     return inc
 
 
-def build(force=False, verbose=False):
+# Development library (tools/ only): -DPL_DEV=1 compiles in the A/B hooks -- environment variables
+# that replace kernel sources or switch on diagnostic (wrong-result) macros -- which the release
+# library above does not contain (tests/test_abi.py checks).  polar_amd._lib.use_dev_library()
+# makes a process load it instead of the release library.
+OBJ_DEV = os.path.join(HERE, "_obj_dev")
+LIB_DEV = os.path.join(HERE, "libpolar_mi355x_dev.so")
+
+
+def build(force=False, verbose=False, dev=False):
     hipcc = _hipcc()
-    os.makedirs(OBJ, exist_ok=True)
+    obj_dir, lib_path = (OBJ_DEV, LIB_DEV) if dev else (OBJ, LIB)
+    dev_flags = ["-DPL_DEV=1"] if dev else []
+    os.makedirs(obj_dir, exist_ok=True)
     inc = _embed_static_source()
     deps = [os.path.join(CSRC, "plan.h"), os.path.join(CSRC, "softplus.h"),
             os.path.join(HERE, "..", "..", "include", "polar_mi355x.h")]
     jobs = []
     for oname, s, defs in UNITS:
         src = os.path.join(CSRC, s)
-        obj = os.path.join(OBJ, oname)
+        obj = os.path.join(obj_dir, oname)
         extra = [inc] if s == "jit.cpp" else []
         if force or _needs(obj, src, deps + extra):
             lang = ["-x", "hip"] if s.endswith(".cpp") else []
             cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-                   "-ffp-contract=off", f"-I{OBJ}", *defs, *lang, "-c", src, "-o", obj]
+                   "-ffp-contract=off", f"-I{OBJ}", *dev_flags, *defs, *lang, "-c", src, "-o", obj]
             jobs.append(cmd)
 
     def run(cmd):
@@ -79,14 +89,15 @@ def build(force=False, verbose=False):
             print(r.stdout + r.stderr)
     with ThreadPoolExecutor(max_workers=min(8, len(jobs) or 1)) as ex:
         list(ex.map(run, jobs))
-    objs = [os.path.join(OBJ, u[0]) for u in UNITS]
-    if force or jobs or not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs):
+    objs = [os.path.join(obj_dir, u[0]) for u in UNITS]
+    if force or jobs or not os.path.exists(lib_path) or \
+            any(os.path.getmtime(o) > os.path.getmtime(lib_path) for o in objs):
         cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, f"-L{ROCM}/lib",
-               f"-Wl,-rpath,{ROCM}/lib", "-lhiprtc", "-o", LIB]
+               f"-Wl,-rpath,{ROCM}/lib", "-lhiprtc", "-o", lib_path]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError("link failed:\n" + r.stdout + r.stderr)
-    return LIB
+    return lib_path
 
 
 def prebuild_codes(codes, workers=None, prune=True):
@@ -211,6 +222,9 @@ def reference_codes():
 
 
 if __name__ == "__main__":
+    if "--dev" in sys.argv:  # the development library only (tools/)
+        print(build(force="--force" in sys.argv, verbose=True, dev=True))
+        sys.exit(0)
     print(build(force="--force" in sys.argv, verbose=True))
     if "--no-kernels" not in sys.argv:
         prebuild_codes(reference_codes())

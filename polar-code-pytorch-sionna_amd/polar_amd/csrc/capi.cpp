@@ -173,14 +173,19 @@ int pl_plan_create(pl_plan** out, int32_t n, const uint8_t* frozen_mask, int32_t
         free_plan(p);
         return r;
     }
-    // SC plans get a kernel specialised to this frozen set (jit.cpp), unless the caller or
-    // PL_SC_SPECIALIZE=0 asks for the generic one.  Failure to specialise is not an error: the
-    // generic kernel is exact too; pl_plan_kernel() reports which one the plan uses.
+    // SC plans get a kernel specialised to this frozen set (jit.cpp) when its code object is in a
+    // kernel cache, unless the caller or PL_SC_SPECIALIZE=0 asks for the generic one.  Compiling a
+    // missing one in this process (hiprtc) is opt-in (PL_PLAN_JIT): in a process that has loaded
+    // another ROCm's amd_comgr (torch's bundled runtime) hiprtc is not reliable (DESIGN.md
+    // section 1), so by default a cache miss leaves the plan on the generic kernel.  Failure to
+    // specialise is not an error: the generic kernel is exact too; pl_plan_kernel() reports which
+    // one the plan uses.
     const char* env = getenv("PL_SC_SPECIALIZE");
     const bool want = list_size == 1 && !(flags & PL_PLAN_GENERIC) && !(env && env[0] == '0');
     if (want) {
         const std::string saved = g_last_error;
-        const int rs = pl::attach_static(p, frozen_mask, !(flags & PL_PLAN_CACHE_ONLY));
+        const bool jit = (flags & PL_PLAN_JIT) && !(flags & PL_PLAN_CACHE_ONLY);
+        const int rs = pl::attach_static(p, frozen_mask, jit);
         if (rs != PL_OK) {
             if (getenv("PL_VERBOSE")) fprintf(stderr, "polar_mi355x: generic SC kernel (%s)\n", g_last_error.c_str());
             pl::detach_static(p);

@@ -135,6 +135,9 @@ constexpr int kWordsPerWave = 256;
 #define PL_AWGN_DIAG 0  // development only (tools/micro/producer_cost.hip): 1 no logit stores,
                         // 2 no noise (Philox + Box-Muller), 3 no Philox for the noise
 #endif  // LDS words per wave: stream words (<= 128) + code words (64)
+#if !PL_DEV && PL_AWGN_DIAG
+#error "PL_AWGN_DIAG gives wrong results: development builds (-DPL_DEV=1) only"
+#endif
 
 __global__ __launch_bounds__(256) void awgn_llr_kernel(int64_t bs, int64_t row0, uint32_t k0, uint32_t k1, uint32_t it,
                                                        float no, const uint32_t* __restrict__ frozen_words, int n, int k,

@@ -143,12 +143,15 @@ std::vector<uint8_t> node_types(int n, const uint8_t* frozen) {
 // n = 2048 already uses the widest group (16 lanes).
 bool tuned_wide(int log_n, int f_mode) { return f_mode == PL_F_MINSUM && log_n >= 8 && log_n <= 10; }
 
-// log2(lanes per codeword); PL_SC_LOG_G overrides it (development A/B: part of the source)
+// log2(lanes per codeword).  Development builds only (PL_DEV, tools/): PL_SC_LOG_G overrides it
+// (A/B of layouts; part of the source, hence of the cache key).
 int static_log_g(int log_n, int f_mode) {
+#if PL_DEV
     if (const char* e = getenv("PL_SC_LOG_G")) {
         const int v = atoi(e);
         if (v >= 0 && v <= 4 && v <= log_n) return v;
     }
+#endif
     if (tuned_wide(log_n, f_mode)) return log_n - 6;
     return log_n > 7 ? log_n - 7 : 0;
 }
@@ -176,8 +179,14 @@ std::string static_source(int n, const uint8_t* frozen, int f_mode) {
     if (tuned_wide(log_n, f_mode)) o << "#define PL_SC_MINW 3\n#define PL_SC_F_BITOP3 1\n";
     const int G = 1 << lg, NS = n >> lg;
     if (NS == 64) o << "#define PL_SC_SIM 1\n";  // the fused Monte-Carlo entry (sc_static.h OUT_SIM)
-    // PL_SC_DEFINES="NAME=VALUE ..." overrides the kernel's tuning macros (development variants;
-    // part of the source, hence of the cache key)
+    std::string body = kStaticSrc;
+#if PL_DEV
+    // Development builds only (PL_DEV, tools/): PL_SC_DEFINES="NAME=VALUE ..." overrides the
+    // kernel's tuning and diagnostic macros, PL_SC_SOURCE=<file> replaces the embedded sc_static.h
+    // (A/B of kernel versions).  Both are part of the source, hence of the cache key; the source
+    // is marked PL_DEV so that sc_static.h accepts its diagnostic (wrong-result) macros.  A
+    // release library reads neither variable.
+    o << "#define PL_DEV 1\n";
     if (const char* defs = getenv("PL_SC_DEFINES")) {
         std::istringstream in(defs);
         std::string tok;
@@ -186,12 +195,11 @@ std::string static_source(int n, const uint8_t* frozen, int f_mode) {
             o << "#define " << tok.substr(0, eq) << " " << (eq == std::string::npos ? "1" : tok.substr(eq + 1)) << "\n";
         }
     }
-    // PL_SC_SOURCE=<file> replaces the embedded sc_static.h (development A/B of kernel versions)
-    std::string body = kStaticSrc;
     if (const char* alt = getenv("PL_SC_SOURCE")) {
         std::vector<char> text;
         if (*alt && read_file(alt, text)) body.assign(text.begin(), text.end());
     }
+#endif
     int k = 0;
     for (int i = 0; i < n; ++i) k += frozen[i] == 0;
     o << body << "\nstruct PlCode {\n  static constexpr int N = " << n << ", K = " << k << ", LOG_N = " << log_n

@@ -70,6 +70,9 @@ constexpr int kWavesPerBlock = 4;
 #ifndef PL_SC_DIAG_NOSTORE
 #define PL_SC_DIAG_NOSTORE 0
 #endif
+#if !PL_DEV && (PL_SC_DIAG_SAMEROW || PL_SC_DIAG_NOSTORE)
+#error "PL_SC_DIAG_* macros give wrong results: development builds (-DPL_DEV=1) only"
+#endif
 #ifndef PL_SC_LOOP_DEPTH
 #define PL_SC_LOOP_DEPTH 3  // nodes with >= 2^depth elements per lane run their children in a loop
 #endif

@@ -46,7 +46,7 @@ typedef unsigned long long uint64_t;
 typedef unsigned long uintptr_t;
 #endif
 
-// Tuning macros (overridable per build; PL_SC_DEFINES in jit.cpp for A/B variants)
+// Tuning macros (overridable per build; development libraries, -DPL_DEV=1, take A/B overrides from jit.cpp)
 #ifndef PL_SC_F_BITOP3
 #define PL_SC_F_BITOP3 0  // A/B on MI355X: 1 (explicit v_bitop3 sign merge) was slower
 #endif
@@ -106,6 +106,11 @@ typedef unsigned long uintptr_t;
 #endif
 #ifndef PL_SC_DIAG_SKIP_SPECIAL
 #define PL_SC_DIAG_SKIP_SPECIAL 0
+#endif
+// Diagnostic macros (timing ablations with WRONG results) exist only in development builds
+// (jit.cpp marks a PL_DEV library's sources with PL_DEV).
+#if !defined(PL_DEV) && (PL_SC_DIAG_SKIP_LANE || PL_SC_DIAG_NO_LOAD || PL_SC_DIAG_NO_TREE || PL_SC_DIAG_SKIP_SPECIAL)
+#error "PL_SC_DIAG_* macros give wrong results: development builds (PL_DEV) only"
 #endif
 #ifndef PL_SC_PERSIST
 #define PL_SC_PERSIST 0  // 1: persistent software-pipelined waves (grid = resident waves)

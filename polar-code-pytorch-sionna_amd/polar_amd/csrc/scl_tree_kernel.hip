@@ -89,6 +89,12 @@ namespace {
 #ifndef PL_SCL_DIAG_NO_COMBINE
 #define PL_SCL_DIAG_NO_COMBINE 0  // timing diagnostic (wrong results)
 #endif
+// Diagnostic macros (timing ablations with WRONG results) exist only in development builds.
+#if !PL_DEV && (PL_SCL_DIAG_NO_UPPER || PL_SCL_DIAG_NO_UPPER_PRUNE || PL_SCL_DIAG_SKIP_V || PL_SCL_DIAG_SKIP_ST || \
+                PL_SCL_DIAG_NO_REPOINT || PL_SCL_DIAG_NO_COMBINE || PL_SCL_DIAG_NO_RANK || PL_SCL_DIAG_CHEAP_PEN || \
+                PL_SCL_DIAG_NO_PULL)
+#error "PL_SCL_DIAG_* macros give wrong results: development builds (-DPL_DEV=1) only"
+#endif
 #ifndef PL_SCL_REPOINT_VEC
 #define PL_SCL_REPOINT_VEC 1  // 1: re-pointing in 16-byte rows, two lanes per (codeword, path) pair (n >= 128)
 #endif
@@ -1378,7 +1384,9 @@ const void* scl_tree_fn<PL_SCL_TREE_L>(int v, bool exact, bool fast) {
 namespace {
 int pick_v(int S) {
     int vmax = 4;  // the channel is read from global memory, so virtual stages cost no LDS
-    if (const char* e = getenv("PL_SCL_VIRTUAL")) vmax = atoi(e);
+#if PL_DEV
+    if (const char* e = getenv("PL_SCL_VIRTUAL")) vmax = atoi(e);  // development A/B (tools/)
+#endif
     if (vmax > 4) vmax = 4;  // instantiated: V = 0..4 (the kernel's layout must match the host's)
     int v = S - 1 - R;
     if (v > vmax) v = vmax;
@@ -1392,8 +1400,10 @@ namespace pl {
 // Eligible plans: 2 <= L <= 32, 32 <= n <= 1024, no fast-SCL pruning.
 bool scl_tree_eligible(const pl_plan* p) {
     if (p->flags & PL_PLAN_GENERIC) return false;
-    if (const char* e = getenv("PL_SCL_TREE_FAST"))  // fast-SCL plans on the generic kernel (A/B)
+#if PL_DEV
+    if (const char* e = getenv("PL_SCL_TREE_FAST"))  // fast-SCL plans on the generic kernel (A/B, tools/)
         if (e[0] == '0' && (p->flags & PL_PLAN_FAST_SCL)) return false;
+#endif
     if (const char* e = getenv("PL_SCL_TREE"))
         if (e[0] == '0') return false;
     return p->list_size >= 2 && p->list_size <= 32 && p->log_n >= 5 && p->log_n <= 10;

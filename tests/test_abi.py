@@ -210,3 +210,44 @@ def test_specialised_source_compiles_for_edge_codes():
     with ThreadPoolExecutor(8) as ex:
         bad = [(j, e) for j, rc, e in ex.map(one, jobs) if rc]
     assert not bad, bad[:2]
+
+
+DEV_HOOKS = ("PL_SC_DEFINES", "PL_SC_SOURCE", "PL_SC_LOG_G", "PL_SCL_VIRTUAL", "PL_SCL_TREE_FAST")
+
+
+def test_release_library_has_no_development_hooks():
+    """The A/B hooks (environment variables that replace kernel sources, change layouts or switch on
+    wrong-result diagnostic macros) are compiled only into libpolar_mi355x_dev.so (-DPL_DEV=1):
+    the release library does not even contain their names, so no environment can reach them."""
+    from polar_amd import _lib
+    blob = open(_lib.LIB_PATH, "rb").read()
+    for name in DEV_HOOKS:
+        assert name.encode() not in blob, name
+    assert b"PL_SC_SPECIALIZE" in blob  # the documented switch (generic kernel, equally exact) stays
+
+
+def test_release_source_ignores_hook_environment(monkeypatch):
+    """The specialised kernel's source (hence its cache key and code object) is the same with the
+    development variables set as without them."""
+    from polar_amd import _lib
+    import polar_amd
+    m = polar_amd.frozen_mask(polar_amd.reference_frozen_pos(512, 1024), 1024)
+    want = _lib.sc_source(1024, m, 0)
+    monkeypatch.setenv("PL_SC_DEFINES", "PL_SC_DIAG_NO_TREE=1")
+    monkeypatch.setenv("PL_SC_SOURCE", HEADER)
+    monkeypatch.setenv("PL_SC_LOG_G", "3")
+    assert _lib.sc_source(1024, m, 0) == want
+    assert "#define PL_DEV" not in want[0] and "PL_SC_DIAG_NO_TREE 1" not in want[0]
+
+
+def test_diagnostic_macros_refuse_release_builds(tmp_path):
+    """A diagnostic (wrong-result) macro without PL_DEV is a compile error in every kernel source."""
+    import subprocess
+    from polar_amd import build as b
+    hipcc = b._hipcc()
+    for src, macro in (("sc_static.h", "PL_SC_DIAG_NO_TREE"), ("scl_tree_kernel.hip", "PL_SCL_DIAG_SKIP_V"),
+                       ("sc_kernel.hip", "PL_SC_DIAG_NOSTORE"), ("channel_kernel.hip", "PL_AWGN_DIAG")):
+        r = subprocess.run([hipcc, "--offload-arch=gfx950", "-std=c++17", "-fsyntax-only", "-x", "hip",
+                            f"-D{macro}=1", f"-I{b.OBJ}", os.path.join(b.CSRC, src)],
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode != 0 and "development builds" in r.stderr, (src, r.stderr[-500:])

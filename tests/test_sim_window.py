@@ -111,3 +111,35 @@ def test_next_window_bounds():
     # a target about to be reached caps the window at the predicted need
     acc = np.array([0, 90, 0, 0])
     assert _next_window(32, 10, 1000, acc, None, 100, 64) == 3
+
+
+def test_counts_argument_is_validated():
+    """ops._counts: the counting kernels' 64-bit atomics only ever see a contiguous int64 tensor of
+    >= 2 elements on the launch device (a caller's counts went straight to the kernel)."""
+    from polar_amd import ops
+    cpu = tc.device("cpu")
+    assert ops._counts(None, cpu).tolist() == [0, 0]
+    ok = tc.zeros(4, dtype=tc.int64)
+    assert ops._counts(ok[:2], cpu) is not None
+    for bad in (tc.zeros(2, dtype=tc.int32), tc.zeros(1, dtype=tc.int64), tc.zeros(4, dtype=tc.int64)[::2],
+                [0, 0], tc.zeros((2, 2), dtype=tc.int64).t()):
+        with pytest.raises(ValueError):
+            ops._counts(bad, cpu)
+    with pytest.raises(ValueError):
+        ops._counts(ok, tc.device("meta"))
+
+
+def test_fused_awgn_stream_keys():
+    """FusedAWGN._draw: stream (point, iteration) -> (iteration, row0 + point << 32); range checks."""
+    from polar_amd import channel, frozen
+    fp = frozen.reference_frozen_pos(32, 64)
+    m = channel.FusedAWGN(64, 32, fp, None, device="cpu", row0=100)
+    assert m._draw(10, (3, 7)) == (7, 100 + (3 << 32))
+    assert m._draw(10, None) == (0, 100) and m._draw(10, None) == (1, 100)  # call order, point 0
+    for stream in ((0, 2 ** 32), (0, -1), (2 ** 31, 0)):
+        with pytest.raises(ValueError):
+            m._draw(10, stream)
+    with pytest.raises(ValueError):
+        m._draw(2 ** 32, (0, 0))
+    with pytest.raises(ValueError):
+        channel.FusedAWGN(64, 32, fp, None, device="cpu", row0=2 ** 32)

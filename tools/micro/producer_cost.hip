@@ -3,7 +3,7 @@
 //   0 as shipped, 1 no logit stores, 2 no noise draw, 3 no Philox for the noise)
 // at (k=512, n=1024), bs = 65536, the packed-bits output of pl_awgn_qpsk_llr_bits; plus a kernel that
 // only writes the same 256 MiB of logits (float4 per lane, 1 KiB per store instruction).
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DPL_AWGN_DIAG=N tools/micro/producer_cost.hip -o ...
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -DPL_DEV=1 -DPL_AWGN_DIAG=N tools/micro/producer_cost.hip -o ...
 #include <cstdio>
 #include <string>
 

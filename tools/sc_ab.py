@@ -21,6 +21,9 @@ VAR = os.path.join(PKG, "polar_amd", "_variants")
 KC = os.path.join(VAR, "kcache")
 SPECS = os.path.join(VAR, "ab.json")
 sys.path.insert(0, PKG)
+from polar_amd import _lib as _pl_lib  # noqa: E402
+
+_pl_lib.use_dev_library()  # the A/B hooks (PL_SC_DEFINES, PL_SC_SOURCE, PL_SC_LOG_G) exist only in the dev build
 
 
 def _env(spec):
@@ -56,6 +59,9 @@ def _load_specs():
 
 def build(names, k, n, fm):
     from concurrent.futures import ThreadPoolExecutor
+
+    from polar_amd import build as _b
+    _b.build(dev=True)
 
     from polar_amd import _lib
     os.makedirs(KC, exist_ok=True)

@@ -13,6 +13,9 @@ VAR = os.path.join(PKG, "polar_amd", "_variants")
 KC = os.path.join(VAR, "kcache")
 SPECS = os.path.join(VAR, "specs.json")
 sys.path.insert(0, PKG)
+from polar_amd import _lib as _pl_lib  # noqa: E402
+
+_pl_lib.use_dev_library()  # the A/B hooks (PL_SC_DEFINES, PL_SC_SOURCE, PL_SC_LOG_G) exist only in the dev build
 
 
 def _env(spec):
@@ -32,8 +35,8 @@ def _mask(k, n):
 
 
 def build(args, k=512, n=1024):
-    import ctypes
-    from polar_amd import _lib
+    from polar_amd import build as _b
+    _b.build(dev=True)
     os.makedirs(KC, exist_ok=True)
     specs = json.load(open(SPECS)) if os.path.exists(SPECS) else {}
     from concurrent.futures import ProcessPoolExecutor
@@ -52,6 +55,7 @@ def _one(job):
     defs, k, n = job
     _env(defs)
     from polar_amd import _lib
+    _lib.use_dev_library()
     m = _mask(k, n)
     buf = ctypes.create_string_buffer(4096)
     rc = _lib.lib().pl_sc_specialize(n, m.ctypes.data_as(ctypes.c_void_p), 0, KC.encode(), buf, 4096)

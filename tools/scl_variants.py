@@ -19,14 +19,14 @@ sys.path.insert(0, PKG)
 
 def build(specs):
     from polar_amd import build as b
-    b.build()
+    b.build(dev=True)  # variants and the baseline: development builds (PL_SCL_VIRTUAL, diagnostic macros)
     os.makedirs(VAR, exist_ok=True)
     hipcc = b._hipcc()
-    objs = [os.path.join(b.OBJ, u[0]) for u in b.UNITS if u[1] != "scl_tree_kernel.hip"]
+    objs = [os.path.join(b.OBJ_DEV, u[0]) for u in b.UNITS if u[1] != "scl_tree_kernel.hip"]
 
     def one(spec):
         name, flags = spec.split(":", 1)
-        base = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", *flags.split()]
+        base = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-DPL_DEV=1", *flags.split()]
         src = os.path.join(b.CSRC, "scl_tree_kernel.hip")
         o1, o2 = os.path.join(VAR, f"sclt_{name}_L8.o"), os.path.join(VAR, f"sclt_{name}_disp.o")
         subprocess.check_call(base + ["-DPL_SCL_TREE_L=8", "-c", src, "-o", o1])
@@ -45,7 +45,8 @@ def time_all(n=1024, k=512, bs=8192, reps=5, rounds=2):
     import torch
     import polar_amd
     from polar_amd import _lib
-    libs = [("default", _lib.LIB_PATH)] + [(f[7:-3], os.path.join(VAR, f)) for f in sorted(os.listdir(VAR))
+    from polar_amd import build as b
+    libs = [("default", b.LIB_DEV)] + [(f[7:-3], os.path.join(VAR, f)) for f in sorted(os.listdir(VAR))
                                            if f.startswith("libscl_") and f.endswith(".so")]
     fp = polar_amd.reference_frozen_pos(k, n).numpy()
     mask = np.ascontiguousarray(polar_amd.frozen_mask(fp, n), dtype=np.uint8)
