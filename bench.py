@@ -65,33 +65,68 @@ def parse():
     return a
 
 
+def cpu_model():
+    """The host CPU's model name (lscpu, else /proc/cpuinfo)."""
+    import subprocess
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=20).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(llr_host, fp, k, n, decoder, L, budget_s):
-    """The pinned C oracle (port of the reference algorithm) on the host cores, bounded sample."""
+    """The pinned C oracle (port of the reference algorithm) on the host cores, bounded sample:
+    all cores (OpenMP) and one core, each the best of 3 timed repetitions on the same LLR rows
+    (BASELINE.md section 3)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     oracle.build()
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or os.cpu_count()
     if decoder == "sc":
-        sample = llr_host[: min(len(llr_host), 65536)]
-        fn = lambda x: oracle.sc_decode(x, fp, nthreads=threads)  # noqa: E731
+        fn = lambda x, t: oracle.sc_decode(x, fp, nthreads=t)  # noqa: E731
+        big, small = llr_host[: min(len(llr_host), 65536)], llr_host[: min(len(llr_host), 4096)]
     else:
-        sample = llr_host[: min(len(llr_host), 4 * threads)]
-        fn = lambda x: oracle.scl_decode(x, fp, L, nthreads=threads, lazy=True)  # noqa: E731
-    fn(sample[: min(len(sample), 256)])  # warm the thread pool
-    done, t0 = 0, time.perf_counter()
-    while True:
-        fn(sample)
-        done += len(sample)
-        if time.perf_counter() - t0 >= budget_s or (decoder == "sc" and done >= 64 * len(sample)):
-            break
-    dt = time.perf_counter() - t0
-    return {"value": round(done / dt / 1e6, 6), "unit": "Mcodewords/s", "cores": threads, "kind": "port",
-            "sample": f"{done} codewords ({len(sample)}-codeword batches of the same AWGN LLRs, "
-                      f"(k={k},n={n}) {decoder.upper()}, oracle/polar_oracle.c OpenMP) in {dt:.1f} s",
-            "reference_cpu_note": ("reference x_run SC_Dec measured in the build container (8 Xeon "
-                                   "threads): 0.00603 Mcodewords/s at this shape (BASELINE.md §2)") if decoder == "sc"
-            else ("reference x_run SCL_Dec (L=8) measured in the build container (8 Xeon threads): "
-                  "6.15e-06 Mcodewords/s at n=1024 (BASELINE.md §2)")}
+        fn = lambda x, t: oracle.scl_decode(x, fp, L, nthreads=t, lazy=True)  # noqa: E731
+        big, small = llr_host[: min(len(llr_host), 4 * threads)], llr_host[: min(len(llr_host), 4)]
+
+    def best_of_3(sample, t, budget):
+        fn(sample[: min(len(sample), 256)], t)  # warm the thread pool and the caches
+        best, done_all, t_all = 0.0, 0, 0.0
+        for _ in range(3):
+            done, t0 = 0, time.perf_counter()
+            while True:
+                fn(sample, t)
+                done += len(sample)
+                if time.perf_counter() - t0 >= budget / 3:
+                    break
+            dt = time.perf_counter() - t0
+            best = max(best, done / dt)
+            done_all, t_all = done_all + done, t_all + dt
+        return best, done_all, t_all
+
+    rate, done, dt = best_of_3(big, threads, 0.7 * budget_s)
+    rate1, done1, dt1 = best_of_3(small, 1, 0.3 * budget_s)
+    ref_note = ("reference x_run SC_Dec measured in the build container (8 Xeon threads): 0.00603 Mcodewords/s "
+                "at this shape, 1 thread 0.00151 Mcodewords/s at bs=8192 (BASELINE.md \u00a72)") if decoder == "sc" \
+        else ("reference x_run SCL_Dec (L=8) measured in the build container (8 Xeon threads): "
+              "6.15e-06 Mcodewords/s at n=1024 (BASELINE.md \u00a72)")
+    return {"value": round(rate / 1e6, 6), "unit": "Mcodewords/s", "cores": threads, "kind": "port",
+            "best_of": 3, "cpu_model": cpu_model(),
+            "sample": f"best of 3 repetitions over {done} codewords ({len(big)}-codeword batches of the same AWGN LLRs, "
+                      f"(k={k},n={n}) {decoder.upper()}, oracle/polar_oracle.c OpenMP, {threads} threads) in {dt:.1f} s",
+            "single_thread": {"value": round(rate1 / 1e6, 6), "unit": "Mcodewords/s", "cores": 1, "best_of": 3,
+                              "sample": f"{done1} codewords ({len(small)}-codeword batches) in {dt1:.1f} s"},
+            "reference_cpu_note": ref_note}
 
 
 def sim_iteration(plan, fp, k, n, bs, ebno, dev, reps=20):
@@ -171,6 +206,39 @@ def sim_iteration(plan, fp, k, n, bs, ebno, dev, reps=20):
 def plan_mask(fp, n):
     import polar_amd
     return polar_amd.frozen_mask(fp, n)
+
+
+VALU_PEAK_GINSTR_S = 1024 * 2.4 / 4  # 256 CUs x 4 SIMDs, one wave64 VALU instruction per 4 cycles at 2.4 GHz
+
+
+def valu_from_profiles(tag):
+    """SQ counters per launch of this shape's kernel from the committed rocprofv3 --pmc pass
+    (profiles/valu.json, written by tools/sq_roofline.py), or None."""
+    path = os.path.join(ROOT, "profiles", "valu.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        return json.load(open(path)).get(tag)
+    except Exception:
+        return None
+
+
+def valu_roofline(tag, kern_ms):
+    """VALU-issue roofline of the kernel: achieved = SQ_INSTS_VALU per launch (wave64 instructions,
+    counted by rocprofv3) / the launch time measured here; peak = 1024 SIMDs issuing one wave64
+    VALU instruction per 4 cycles at 2.4 GHz; busy_frac = SQ_ACTIVE_INST_VALU (quad-cycles a wave
+    spends issuing VALU work) x 4 / (1024 x 2.4 GHz x launch time)."""
+    v = valu_from_profiles(tag)
+    if not v:
+        return None
+    t = kern_ms * 1e-3
+    ach = v["sq_insts_valu_per_launch"] / t / 1e9
+    out = {"bound": "valu", "achieved": round(ach, 2), "peak": VALU_PEAK_GINSTR_S, "unit": "G wave-instr/s",
+           "frac": round(ach / VALU_PEAK_GINSTR_S, 5), "kernel_ms": round(kern_ms, 5),
+           "valu_instr_per_launch": v["sq_insts_valu_per_launch"], "counter_file": v.get("source")}
+    if v.get("sq_active_inst_valu_per_launch"):
+        out["busy_frac"] = round(v["sq_active_inst_valu_per_launch"] * 4 / (1024 * 2.4e9 * t), 5)
+    return out
 
 
 def traffic_from_profiles(tag):
@@ -309,6 +377,14 @@ def main():
                          "kernel_ms": round(kern_ms, 5), "algorithmic_bytes_per_launch": bytes_per_launch},
             "cpu_baseline": cpu,
         }
+        rv = valu_roofline(tag, kern_ms)
+        if a.decoder == "scl" and rv is not None:
+            # the list decoder is bound by VALU issue and leaf latency (0.6 % of HBM): its roofline is
+            # the VALU one, the HBM figure stays next to it
+            line["roofline_hbm"] = line["roofline"]
+            line["roofline"] = rv
+        elif rv is not None:
+            line["roofline_valu"] = rv
         if sim_it is not None:
             line["sim_iteration"] = sim_it
         print(json.dumps(line), flush=True)

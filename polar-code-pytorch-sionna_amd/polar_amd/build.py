@@ -45,6 +45,9 @@ def _needs(obj, src, deps):
 def _embed_static_source():
     """sc_static.h as a C++ raw string literal (the hiprtc source of the specialised kernels)."""
     src = open(os.path.join(CSRC, "sc_static.h")).read()
+    inc_line = '#include "exactf.h"  // build.py inlines it into the embedded source\n'
+    assert inc_line in src
+    src = src.replace(inc_line, open(os.path.join(CSRC, "exactf.h")).read().replace("#pragma once\n", ""))
     assert ")PLSRC\"" not in src
     inc = os.path.join(OBJ, "sc_static_src.inc")
     text = 'R"PLSRC(' + src + ')PLSRC"\n'
@@ -68,7 +71,7 @@ def build(force=False, verbose=False, dev=False):
     dev_flags = ["-DPL_DEV=1"] if dev else []
     os.makedirs(obj_dir, exist_ok=True)
     inc = _embed_static_source()
-    deps = [os.path.join(CSRC, "plan.h"), os.path.join(CSRC, "softplus.h"),
+    deps = [os.path.join(CSRC, "plan.h"), os.path.join(CSRC, "softplus.h"), os.path.join(CSRC, "exactf.h"),
             os.path.join(HERE, "..", "..", "include", "polar_mi355x.h")]
     jobs = []
     for oname, s, defs in UNITS:
@@ -132,10 +135,10 @@ def prebuild_codes(codes, workers=None, prune=True):
 
 def test_random_codes():
     """The arbitrary frozen sets tests/test_sc_gpu.py::test_sc_random_vs_oracle decodes with the
-    specialised kernel (n <= 256, same seeds), so the GPU tests never compile."""
+    specialised kernel (every n = 2 ... 2048, same seeds), so the GPU tests never compile."""
     import numpy as np
     out = []
-    for log_n in range(1, 9):
+    for log_n in range(1, 12):
         for rate in (0.25, 0.5, 0.75):
             n = 1 << log_n
             rng = np.random.default_rng(log_n * 10 + int(rate * 4))

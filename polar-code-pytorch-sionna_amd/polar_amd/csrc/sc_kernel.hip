@@ -31,6 +31,7 @@
 #include <type_traits>
 
 #include "../../../include/polar_mi355x.h"
+#include "exactf.h"
 #include "plan.h"
 
 namespace {
@@ -100,11 +101,8 @@ __device__ __forceinline__ float fop(float x, float y, float lmax) {
         const float m = fminf(fminf(fabsf(x), fabsf(y)), lmax);
         const uint32_t sg = (__float_as_uint(x) ^ __float_as_uint(y)) & 0x80000000u;
         return __uint_as_float(__float_as_uint(m) | sg);
-    } else {  // my_sn/fec/polar/dec.py:39-43
-        const float xc = fminf(fmaxf(x, -lmax), lmax), yc = fminf(fmaxf(y, -lmax), lmax);
-        float o = logf(1.0f + expf(xc + yc));
-        o -= logf(expf(xc) + expf(yc));
-        return o;
+    } else {  // my_sn/fec/polar/dec.py:39-43, correctly rounded exp / log (exactf.h)
+        return plx::f_exact(x, y, lmax);
     }
 }
 // g, polar_sc.py:49-53: (1-2u)x + y == (u ? -x : x) + y, one rounding.

@@ -45,6 +45,7 @@ typedef long long int64_t;
 typedef unsigned long long uint64_t;
 typedef unsigned long uintptr_t;
 #endif
+#include "exactf.h"  // build.py inlines it into the embedded source
 
 // Tuning macros (overridable per build; development libraries, -DPL_DEV=1, take A/B overrides from jit.cpp)
 #ifndef PL_SC_F_BITOP3
@@ -231,10 +232,7 @@ __device__ __forceinline__ float fop(float x, float y, float lmax) {
         return uf(fu(m) | ((fu(x) ^ fu(y)) & 0x80000000u));
 #endif
     } else {
-        const float xc = fminf(fmaxf(x, -lmax), lmax), yc = fminf(fmaxf(y, -lmax), lmax);
-        float o = logf(1.0f + expf(xc + yc));
-        o -= logf(expf(xc) + expf(yc));
-        return o;
+        return plx::f_exact(x, y, lmax);  // my_sn dec.py:39-43, correctly rounded exp / log (exactf.h)
     }
 }
 // g, polar_sc.py:49-53: (1-2u)x + y == (u ? -x : x) + y, one rounding.  The flip is the sign
@@ -629,12 +627,20 @@ __device__ __forceinline__ BV<(1 << s) / C::G> node(const float (&a)[(1 << s) / 
 // stage LOG_N-1 buffers are "virtual": each of their LLRs is recomputed from two channel values
 // when a pass of the stage-(LOG_N-1) node reads it (f for the left half, g with the left half's
 // partial sums for the right), so the largest stage buffer never occupies registers.
-// f(-x,-y) = f(x,y) and g(-x,-y) = -g(x,y): the negation of polar_sc.py:122 costs nothing (the
-// sign of an exact zero is never observable: every decision treats +0 and -0 alike).
+// Min-sum f(-x,-y) = f(x,y) bit for bit and g(-x,-y) = -g(x,y): the negation of polar_sc.py:122
+// costs nothing (the sign of an exact zero is never observable: every decision treats +0 and -0
+// alike).  The exact boxplus is only algebraically even -- log(1+e^(x+y)) - log(e^x+e^y) rounds
+// differently from the same formula on -x, -y (dec.py:39-43 evaluates it on the negated channel,
+// dec.py:147) -- so FM = 1 negates first (source modifiers, no extra instruction).
+template <class C>
+__device__ __forceinline__ float vfroot(float x, float y, float lmax) {
+    if constexpr (C::FM == 0) return fop<0>(x, y, lmax);
+    else return fop<C::FM>(-x, -y, lmax);
+}
 template <class C>
 __device__ __forceinline__ float valpha(const float (&ch)[C::NS], int side, uint64_t blr, int j, float lmax) {
     const float x = ch[j], y = ch[j + C::NS / 2];
-    return side == 0 ? fop<C::FM>(x, y, lmax) : (-flip31(x, bit31(blr, j))) - y;
+    return side == 0 ? vfroot<C>(x, y, lmax) : (-flip31(x, bit31(blr, j))) - y;
 }
 
 // all NS/2 virtual stage-(LOG_N-1) LLRs of one half
@@ -1269,7 +1275,7 @@ __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs
         if constexpr (nt<C>(C::LOG_N - 1, 0) != R0) {
             float a[E];
 #pragma unroll
-            for (int j = 0; j < E; ++j) a[j] = fop<C::FM>(ch[j * G + res], ch[(j + E) * G + res], lmax);
+            for (int j = 0; j < E; ++j) a[j] = vfroot<C>(ch[j * G + res], ch[(j + E) * G + res], lmax);
             if constexpr (E == 1) bl = lnode<C, C::LOG_N - 1, 0>(a[0], ln) >> 31;
             else bl = packed(node<C, C::LOG_N - 1, 0>(a, ln));
         }

@@ -93,10 +93,19 @@ def test_sim_ber_fused_equals_two_kernel_path(pa):
     from polar_amd import channel, sim
     k, n = 512, 1024
     fp = pa.reference_frozen_pos(k, n)
+    class ForwardOnly:  # the same keyed draws through forward() + pl_count_errors (no error_counts)
+        keyed_streams = True
+
+        def __init__(self, m):
+            self.m = m
+
+        def __call__(self, batch_size, ebno_db, stream=None):
+            return self.m(batch_size, ebno_db, stream=stream)
+
     counts = []
     for fused in (True, False):
         model = channel.FusedAWGN(n, k, fp, pa.SC_Dec(fp, n), seed=3, sim_kernel=False)
-        mc = model if fused else (lambda batch_size, ebno_db, m=model: m(batch_size, ebno_db))
+        mc = model if fused else ForwardOnly(model)
         _, _, cnt = sim.sim_ber(mc, [2.5, 3.0, 3.5], 8192, 3, verbose=False, device="cuda", return_counts=True)
         counts.append(cnt)
     assert torch.equal(counts[0], counts[1]), counts

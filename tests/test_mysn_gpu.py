@@ -3,14 +3,17 @@
   polar_amd.mysn.SCL_Dec <-> my_sn/fec/polar/dec.py:158-537 (exact f, fast-SCL, CRC-aided pick)
   polar_amd.mysn.SC_Dec  <-> my_sn/fec/polar/dec.py:13-157  (exact f)
 
-The exact boxplus f is log/exp arithmetic, so the GPU (ocml) and the reference (numpy) differ in
-the last ulp; as for exact-f SC (tests/test_sc_gpu.py) the bits are gated on agreement rate, here
-against both the reference fixtures and the C oracle (glibc), with path metrics within 1e-6 on
-agreeing rows.  The CRC-aided pick and the fast-SCL node sums (numpy pairwise order) are exact
-given the same metrics.
+The exact boxplus f is log/exp arithmetic, so the GPU (ocml fp64) and the reference (numpy) can
+differ in the last ulp; the bits are gated by a one-sided binomial test on the row-mismatch count
+(level 1e-3) at the rate tests/test_exactf_gpu.py establishes with 5,000 reference rows
+(P0_SCL = 6e-4, the 95 % bound of the C oracle's own rate there), against both the reference
+fixtures and the C oracle (glibc), with path metrics within 1e-6 on agreeing rows.  The
+CRC-aided pick and the fast-SCL node sums (numpy pairwise order) are exact given the same
+metrics.
 """
 import glob
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -20,6 +23,11 @@ import oracle
 
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+sys.path.insert(0, GOLDEN)
+from exactf_recipe import binom_upper_ok  # noqa: E402
+
+P0_SCL = 6e-4  # exact-f SCL row-mismatch rate gate (tests/test_exactf_gpu.py: the oracle's 95 % bound)
+P0_SC = 1e-4  # exact-f SC
 CASES = [("mysn_scl_L8_32_64", {}), ("mysn_scl_L8_128_256", {}), ("mysn_scl_nofast_L4_32_64", {"fast": False}),
          ("mysn_scl_crc11_L8_32_64", {"crc": "CRC11"}), ("mysn_scl_crc24c_L8_128_256", {"crc": "CRC24C"})]
 
@@ -47,17 +55,17 @@ def test_mysn_scl_golden(pa, fname, kw):
         rows += len(ok)
         agree += int(ok.sum())
         assert np.abs(pm[ok] - d["pm_stable_" + name][ok]).max() < 1e-6, name
-    assert agree / rows >= 0.97, (agree, rows)
+    assert binom_upper_ok(rows - agree, rows, P0_SCL), (agree, rows)
 
 
 @pytest.mark.parametrize("log_n", [3, 5, 6, 7, 8, 9, 10])
 @pytest.mark.parametrize("L", [2, 8])
 @pytest.mark.parametrize("fast", [True, False])
 def test_mysn_scl_random_code_vs_oracle(pa, log_n, L, fast):
-    """Arbitrary frozen sets.  Min-sum f: bit-exact and metrics to 1e-9.  Exact f: gated on
-    agreement rate over AWGN codewords -- the exact f is so ulp-sensitive that re-running the
-    oracle itself with long-double f changes 10-22 % of rows on high-variance random LLRs and
-    0-3 % on AWGN codewords, so only the rate is meaningful there."""
+    """Arbitrary frozen sets.  Min-sum f: bit-exact and metrics to 1e-9, on AWGN codewords with
+    every 9th LLR rounded (exact ties and zeros).  Exact f: on the unrounded AWGN codewords (a
+    rounded LLR makes f's cancellation decide by the last ulp), row mismatches against the
+    oracle within the binomial gate at P0_SCL, metrics to 1e-6 on agreeing rows."""
     from polar_amd import _lib, ops
     n = 1 << log_n
     if n * L > 4096:
@@ -68,7 +76,8 @@ def test_mysn_scl_random_code_vs_oracle(pa, log_n, L, fast):
     bs = 37
     u = rng.integers(0, 2, (bs, k)).astype(np.float32)
     cw = oracle.polar_encode(u, fp, n)
-    llr = ((2 * cw - 1) * 2.0 + rng.standard_normal(cw.shape) * 1.4).astype(np.float32)
+    llr_awgn = ((2 * cw - 1) * 2.0 + rng.standard_normal(cw.shape) * 1.4).astype(np.float32)
+    llr = llr_awgn.copy()
     llr[:, ::9] = np.round(llr[:, ::9])  # exact ties and zeros
     flags = _lib.PL_PLAN_FAST_SCL if fast else 0
     want, wpm = oracle.scl_decode_mysn(llr, fp, L, fast_scl=fast, exact_f=False)
@@ -76,11 +85,11 @@ def test_mysn_scl_random_code_vs_oracle(pa, log_n, L, fast):
     got, pm = ops.scl_decode(plan, torch.from_numpy(llr).cuda(), return_pm=True)
     assert np.array_equal(got.cpu().numpy(), want)
     assert np.abs(pm.cpu().numpy() - wpm).max() < 1e-9
-    want, wpm = oracle.scl_decode_mysn(llr, fp, L, fast_scl=fast, exact_f=True)
+    want, wpm = oracle.scl_decode_mysn(llr_awgn, fp, L, fast_scl=fast, exact_f=True)
     plan = _lib.Plan(n, pa.frozen_mask(fp, n), L, _lib.PL_F_EXACT, flags=flags)
-    got, pm = ops.scl_decode(plan, torch.from_numpy(llr).cuda(), return_pm=True)
+    got, pm = ops.scl_decode(plan, torch.from_numpy(llr_awgn).cuda(), return_pm=True)
     ok = (got.cpu().numpy() == want).all(1)
-    assert ok.mean() >= 0.85, ok.mean()
+    assert binom_upper_ok(int((~ok).sum()), len(ok), P0_SCL), ok.mean()
     assert np.abs(pm.cpu().numpy()[ok] - wpm[ok]).max() < 1e-6
 
 
@@ -144,7 +153,7 @@ def test_mysn_sc_module(pa):
     dec = mysn.SC_Dec(torch.from_numpy(d["frozen_pos"].astype(np.int64)), 256)
     got = dec(torch.from_numpy(d["llr_awgn2"])).numpy().astype(np.uint8)
     assert got.shape == d["exact_awgn2"].shape
-    assert (got != d["exact_awgn2"]).any(1).mean() <= 0.02
+    assert binom_upper_ok(int((got != d["exact_awgn2"]).any(1).sum()), len(got), P0_SC)
 
 
 @pytest.mark.parametrize("kernel", ["subtree", "generic"])
@@ -173,7 +182,7 @@ def test_mysn_scl_crc_llr_max_vs_oracle(pa, kernel, fast):
     assert (wpm.max(1) >= lmax * k).any()
 
 
-@pytest.mark.parametrize("L", [2, 8, 16])
+@pytest.mark.parametrize("L", [2, 4, 8, 16])
 @pytest.mark.parametrize("fast", [False, True])
 def test_scl_n2048_vs_oracle(pa, L, fast):
     """n = 2048 list decoding (generic kernel, list state in LDS up to L = 16): min-sum f,
@@ -183,7 +192,7 @@ def test_scl_n2048_vs_oracle(pa, L, fast):
     n, k = 2048, 1024
     fp = pa.reference_frozen_pos(k, n).numpy()
     rng = np.random.default_rng(L + 3 * fast)
-    bs = 6 if L == 16 else 12
+    bs = 6 if L >= 8 else 12
     u = rng.integers(0, 2, (bs, k)).astype(np.float32)
     cw = oracle.polar_encode(u, fp, n)
     llr = ((2 * cw - 1) * 1.8 + rng.standard_normal(cw.shape) * 1.3).astype(np.float32)

@@ -5,13 +5,14 @@
     codewords bit-identical to the reference's.
   * Polar5GDecoder rate recovery (pl_rate_recover): the mother-code LLRs bit-identical to the
     ones the reference hands its decoder (captured in the fixture).
-  * Decoding: the mother decoders are my_sn's exact-f SC / SCL (exp/log arithmetic), gated like
-    tests/test_mysn_gpu.py on the agreement rate with the reference's decoded bits, and exact on
-    noiseless round trips.
+  * Decoding: the mother decoders are my_sn's exact-f SC / SCL (exp/log arithmetic), gated by a
+    binomial test on the row-mismatch count against the reference's decoded bits (the rates of
+    tests/test_exactf_gpu.py), and exact on noiseless round trips.
 """
 import contextlib
 import io
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -70,10 +71,13 @@ def test_rate_recovery_gpu_vs_reference(g):
 
 @pytest.mark.parametrize("dec_type", ["SC", "SCL"])
 def test_decoder_vs_reference(g, dec_type):
-    """Agreement with the reference's decoded bits over the uplink fixtures.  Excluded: the
-    rate-1 mother code ((1013, 1088): k_polar = n_polar = 1024, no frozen bit), where every
-    decision is the sign of an exact-f chain decided by last-ulp rounding -- the C oracle (glibc
-    exp/log) agrees with the reference (numpy/SLEEF) on only 4 of its 24 rows."""
+    """Row mismatches against the reference's decoded bits over the uplink fixtures, within the
+    one-sided binomial gate (level 1e-3) at the rates tests/test_exactf_gpu.py establishes with
+    85,000 / 6,000 reference rows (SC 1e-4, SCL 5e-4).  The rate-1 mother code ((1013, 1088):
+    k_polar = n_polar = 1024, no frozen bit) is gated there against the oracle's own rate (~9 % of
+    its rows are decided by last-ulp rounding even between glibc and the reference), not here."""
+    sys.path.insert(0, GOLDEN)
+    from exactf_recipe import binom_upper_ok
     from polar_amd import polar5g
     rows = agree = 0
     for k, n in _cases(g, "ul"):
@@ -88,7 +92,7 @@ def test_decoder_vs_reference(g, dec_type):
         ok = (out.numpy().astype(np.uint8) == g[key]).all(1)
         rows += len(ok)
         agree += int(ok.sum())
-    assert rows > 0 and agree / rows >= 0.97, (agree, rows)
+    assert rows > 0 and binom_upper_ok(rows - agree, rows, 1e-4 if dec_type == "SC" else 5e-4), (agree, rows)
 
 
 @pytest.mark.parametrize("dec_type", ["SC", "SCL"])

@@ -10,6 +10,7 @@ reference codes, compiled with hiprtc at plan time for any other code) and the g
 """
 import glob
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -33,7 +34,8 @@ KINDS = ("specialized", "generic")
 
 def _plan(pa, fp, n, f_mode=0, L=1, kind="specialized"):
     from polar_amd import _lib
-    flags = _lib.PL_PLAN_GENERIC if kind == "generic" else 0
+    # specialised: only pre-built code objects (build.py), never a compile on the GPU box
+    flags = _lib.PL_PLAN_GENERIC if kind == "generic" else _lib.PL_PLAN_CACHE_ONLY
     plan = _lib.Plan(n, pa.frozen_mask(fp, n), L, f_mode, flags=flags)
     assert plan.kernel()[0] == kind, plan.kernel()
     return plan
@@ -61,8 +63,8 @@ def test_sc_golden_bit_exact(pa, path, kind):
 @pytest.mark.parametrize("log_n", list(range(1, 12)))
 @pytest.mark.parametrize("rate", [0.25, 0.5, 0.75])
 def test_sc_random_vs_oracle(pa, log_n, rate, kind):
-    if kind == "specialized" and log_n > 8:
-        pytest.skip("hiprtc compile per random code; large n covered by the reference codes")
+    """Arbitrary frozen sets at every n = 2 ... 2048 and three rates, both SC kernels (the
+    specialised ones are pre-built by build.test_random_codes, so nothing compiles on the box)."""
     n = 1 << log_n
     rng = np.random.default_rng(log_n * 10 + int(rate * 4))
     k = max(1, int(n * rate))
@@ -176,15 +178,24 @@ def test_sc_dropin_module_matches_reference_contract(pa):
 
 @pytest.mark.parametrize("kind", KINDS)
 def test_sc_exact_mode_statistical(pa, kind):
+    """Exact-boxplus SC (my_sn dec.py:39-43) on the golden shapes' AWGN and saturation sets:
+    row mismatches against the reference within the one-sided binomial gate at rate 1e-4
+    (the statistical-power version is tests/test_exactf_gpu.py).  The
+    random N(0, 4) sets are left out: there the cancellation in f decides ~4 % of rows by the
+    last ulp even between two correctly rounded libms (the C oracle: 59 of 1440)."""
+    sys.path.insert(0, GOLDEN)
+    from exactf_recipe import binom_upper_ok
+    mism = rows = 0
     for path in sorted(glob.glob(os.path.join(GOLDEN, "sc_*.npz"))):
         d = np.load(path)
         plan = _plan(pa, d["frozen_pos"], int(d["n"]), f_mode=1, kind=kind)
         for name in _sets(d):
-            if not name.startswith("awgn"):
+            if not (name.startswith("awgn") or name == "sat"):
                 continue
             got = pa.ops.sc_decode(plan, torch.from_numpy(d["llr_" + name]).cuda()).cpu().numpy().astype(np.uint8)
-            rate = float((got != d["exact_" + name]).any(1).mean())
-            assert rate <= 0.02, (path, name, rate)
+            mism += int((got != d["exact_" + name]).any(1).sum())
+            rows += len(got)
+    assert rows >= 2000 and binom_upper_ok(mism, rows, 1e-4), (mism, rows)
 
 
 def test_sc_specialized_jit_for_an_arbitrary_code(pa, tmp_path, monkeypatch):
