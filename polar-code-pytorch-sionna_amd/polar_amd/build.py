@@ -218,6 +218,8 @@ def reference_codes():
         out += polar5g_codes()
     out += test_random_codes()
     out += [(m, 0) for _, m in root_half_codes()]
+    # tests/test_sc_gpu.py::test_sc_edge_cases: n = 64 with every position frozen (k = 0) and none (k = n)
+    out += [(np.ones(64, dtype=np.uint8), 0), (np.zeros(64, dtype=np.uint8), 0)]
     uniq = {}
     for m, fm in out:
         uniq[(bytes(bytearray(m)), fm)] = (m, fm)

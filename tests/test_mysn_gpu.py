@@ -63,9 +63,13 @@ def test_mysn_scl_golden(pa, fname, kw):
 @pytest.mark.parametrize("fast", [True, False])
 def test_mysn_scl_random_code_vs_oracle(pa, log_n, L, fast):
     """Arbitrary frozen sets.  Min-sum f: bit-exact and metrics to 1e-9, on AWGN codewords with
-    every 9th LLR rounded (exact ties and zeros).  Exact f: on the unrounded AWGN codewords (a
-    rounded LLR makes f's cancellation decide by the last ulp), row mismatches against the
-    oracle within the binomial gate at P0_SCL, metrics to 1e-6 on agreeing rows."""
+    every 9th LLR rounded (exact ties and zeros).  Exact f: row mismatches against the oracle
+    within the binomial gate at P0_SCL, metrics to 1e-6 on agreeing rows -- on unrounded AWGN
+    codewords of random codes that freeze at least the n/4 least reliable positions.  (With an
+    information bit at one of those, its LLR after log2(n) exact-f levels is rounding noise of
+    the f formula, e.g. ~1e-16 of either sign, and the list's choice is decided by it: the C
+    oracle itself changes 30-75 % of such rows at n = 1024 when 1/4 of its fp64 exp/log results
+    move by one ulp, and 0-1 of 37 on these codes.)"""
     from polar_amd import _lib, ops
     n = 1 << log_n
     if n * L > 4096:
@@ -76,8 +80,7 @@ def test_mysn_scl_random_code_vs_oracle(pa, log_n, L, fast):
     bs = 37
     u = rng.integers(0, 2, (bs, k)).astype(np.float32)
     cw = oracle.polar_encode(u, fp, n)
-    llr_awgn = ((2 * cw - 1) * 2.0 + rng.standard_normal(cw.shape) * 1.4).astype(np.float32)
-    llr = llr_awgn.copy()
+    llr = ((2 * cw - 1) * 2.0 + rng.standard_normal(cw.shape) * 1.4).astype(np.float32)
     llr[:, ::9] = np.round(llr[:, ::9])  # exact ties and zeros
     flags = _lib.PL_PLAN_FAST_SCL if fast else 0
     want, wpm = oracle.scl_decode_mysn(llr, fp, L, fast_scl=fast, exact_f=False)
@@ -85,6 +88,10 @@ def test_mysn_scl_random_code_vs_oracle(pa, log_n, L, fast):
     got, pm = ops.scl_decode(plan, torch.from_numpy(llr).cuda(), return_pm=True)
     assert np.array_equal(got.cpu().numpy(), want)
     assert np.abs(pm.cpu().numpy() - wpm).max() < 1e-9
+    base = pa.reference_frozen_pos(n - n // 4, n).numpy()  # the n/4 least reliable positions (froze.py)
+    fp = np.sort(np.concatenate([base, rng.choice(np.setdiff1d(np.arange(n), base), n // 4, replace=False)]))
+    cw = oracle.polar_encode(u, fp, n)
+    llr_awgn = ((2 * cw - 1) * 2.0 + rng.standard_normal(cw.shape) * 1.4).astype(np.float32)
     want, wpm = oracle.scl_decode_mysn(llr_awgn, fp, L, fast_scl=fast, exact_f=True)
     plan = _lib.Plan(n, pa.frozen_mask(fp, n), L, _lib.PL_F_EXACT, flags=flags)
     got, pm = ops.scl_decode(plan, torch.from_numpy(llr_awgn).cuda(), return_pm=True)

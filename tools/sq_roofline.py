@@ -22,7 +22,7 @@ KEYS = {"sc": "sc_k512_n1024_bs65536", "scl": "scl_k512_n1024_bs8192_L8"}
 
 
 def kname(raw):
-    return re.sub(r"^void (\(anonymous namespace\)::)?", "", raw).split("(")[0]
+    return re.sub(r"^(void )?(\(anonymous namespace\)::)?", "", raw.strip()).split("(")[0]
 
 
 def per_dispatch(path, kernel):

@@ -16,7 +16,7 @@ import re
 
 
 def kname(raw):
-    return re.sub(r"^void (\(anonymous namespace\)::)?", "", raw).split("(")[0]
+    return re.sub(r"^(void )?(\(anonymous namespace\)::)?", "", raw.strip()).split("(")[0]
 
 
 def main():
