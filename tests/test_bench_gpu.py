@@ -29,9 +29,15 @@ def test_bench_json_contract(decoder):
     assert d["n_gpus"] == 1 and d["steps"] == 5 and d["scaling"] == "weak" and d["higher_is_better"] is True
     assert d["value"] > 0 and d["unit"] == "Mcodewords/s"
     assert d["config"]["kernel"] in ("specialized", "scl_subtree")
-    rf = d["roofline"]
+    rf = d["roofline"] if decoder == "sc" else d["roofline_hbm"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-4
+    # the VALU-issue roofline from the committed SQ counters (profiles/valu.json): the list
+    # decoder's own bound; next to the HBM one for SC
+    rv = d["roofline"] if decoder == "scl" else d["roofline_valu"]
+    assert rv["bound"] == "valu" and rv["unit"] == "G wave-instr/s" and 0 < rv["frac"] < 1.2
+    assert abs(rv["frac"] - rv["achieved"] / rv["peak"]) < 1e-4 and rv["counter_file"]
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1 and cb["sample"]
+    assert cb["best_of"] == 3 and cb["single_thread"]["cores"] == 1 and cb["single_thread"]["value"] > 0
     assert d["dtype"] == ("f32" if decoder == "sc" else "f64")
