@@ -89,11 +89,20 @@ __device__ __forceinline__ double f_ms(double x, double y, double lmax) {  // po
     const bool neg = (__double_as_longlong(x) ^ __double_as_longlong(y)) < 0;
     return neg ? -m : m;
 }
+#ifndef PL_SCL_FEX_FORM
+#define PL_SCL_FEX_FORM 1  // exact f: 1 = softplus.h f_exact_pm (no cancellation), 0 = the reference's expression (ocml)
+#endif
 __device__ __forceinline__ double f_ex(double x, double y, double lmax) {  // my_sn dec.py:330-339
+#if PL_SCL_DIAG_FMS_ALL  // timing diagnostic only (wrong results): min-sum in place of the exact f
+    return fmin(fmin(fabs(x), fabs(y)), lmax) * (((x < 0) != (y < 0)) ? -1.0 : 1.0);
+#elif PL_SCL_FEX_FORM == 0
     const double xc = fmax(fmin(x, lmax), -lmax), yc = fmax(fmin(y, lmax), -lmax);
     double o = log(1.0 + exp(xc + yc));
     o -= log(exp(xc) + exp(yc));
     return o;
+#else
+    return pl::f_exact_pm(x, y, lmax);  // softplus.h: the same value without the cancellation
+#endif
 }
 template <int FM>
 __device__ __forceinline__ double f_op(double x, double y, double lmax) {

@@ -92,7 +92,7 @@ namespace {
 // Diagnostic macros (timing ablations with WRONG results) exist only in development builds.
 #if !PL_DEV && (PL_SCL_DIAG_NO_UPPER || PL_SCL_DIAG_NO_UPPER_PRUNE || PL_SCL_DIAG_SKIP_V || PL_SCL_DIAG_SKIP_ST || \
                 PL_SCL_DIAG_NO_REPOINT || PL_SCL_DIAG_NO_COMBINE || PL_SCL_DIAG_NO_RANK || PL_SCL_DIAG_CHEAP_PEN || \
-                PL_SCL_DIAG_NO_PULL)
+                PL_SCL_DIAG_NO_PULL || PL_SCL_DIAG_FMS_ALL)
 #error "PL_SCL_DIAG_* macros give wrong results: development builds (-DPL_DEV=1) only"
 #endif
 #ifndef PL_SCL_REPOINT_VEC
@@ -168,11 +168,20 @@ __device__ __forceinline__ double f_ms(double x, double y, double lmax) {  // po
     return neg ? -m : m;
 #endif
 }
+#ifndef PL_SCL_FEX_FORM
+#define PL_SCL_FEX_FORM 1  // exact f: 1 = softplus.h f_exact_pm (no cancellation), 0 = the reference's expression (ocml)
+#endif
 __device__ __forceinline__ double f_ex(double x, double y, double lmax) {  // my_sn dec.py:330-339
+#if PL_SCL_DIAG_FMS_ALL  // timing diagnostic only (wrong results): min-sum in place of the exact f
+    return fmin(fmin(fabs(x), fabs(y)), lmax) * (((x < 0) != (y < 0)) ? -1.0 : 1.0);
+#elif PL_SCL_FEX_FORM == 0
     const double xc = fmax(fmin(x, lmax), -lmax), yc = fmax(fmin(y, lmax), -lmax);
     double o = log(1.0 + exp(xc + yc));
     o -= log(exp(xc) + exp(yc));
     return o;
+#else
+    return pl::f_exact_pm(x, y, lmax);  // softplus.h: the same value without the cancellation
+#endif
 }
 template <int FM>
 __device__ __forceinline__ double f_op(double x, double y, double lmax) {
