@@ -98,6 +98,9 @@ namespace {
 #ifndef PL_SCL_REPOINT_VEC
 #define PL_SCL_REPOINT_VEC 1  // 1: re-pointing in 16-byte rows, two lanes per (codeword, path) pair (n >= 128)
 #endif
+#ifndef PL_SCL_FEX_HOIST
+#define PL_SCL_FEX_HOIST 1  // 1: exact-f virtual passes evaluate the path-independent f levels once (vvisit_ex)
+#endif
 #ifndef PL_SCL_WPE
 #define PL_SCL_WPE 2  // > 0: amdgpu_waves_per_eu minimum (2: <= 256 VGPRs, A/B on MI355X: 2.30 vs 3.62 ms at V=4)
 #endif
@@ -181,6 +184,19 @@ __device__ __forceinline__ double f_ex(double x, double y, double lmax) {  // my
     return o;
 #else
     return pl::f_exact_pm(x, y, lmax);  // softplus.h: the same value without the cancellation
+#endif
+}
+// two exact f evaluations interleaved (independent chains overlap within the wave)
+__device__ __forceinline__ void f_ex2(double x0, double y0, double x1, double y1, double lmax, double& r0, double& r1) {
+#if PL_SCL_DIAG_FMS_ALL || PL_SCL_FEX_FORM == 0
+    r0 = f_ex(x0, y0, lmax);
+    r1 = f_ex(x1, y1, lmax);
+#else
+    const double x[2] = {x0, x1}, y[2] = {y0, y1};
+    double r[2];
+    pl::f_exact_pm_n<2>(x, y, lmax, r);
+    r0 = r[0];
+    r1 = r[1];
 #endif
 }
 template <int FM>
@@ -527,6 +543,129 @@ __device__ void vvisit64(const St& t, int pos, bool is_g, int lane, const int* w
     }
 }
 
+// One pass of a virtual node for the exact f (FM = 1, any V >= 1), where an f costs ~70 VALU and
+// dominates: the leading f levels (from the channel down to the first g) are path-independent, so
+// each lane evaluates them once per (codeword, element) and only the levels below the first g
+// once per path -- 2.1x fewer f evaluations than the per-path recursion at n = 1024.  Every level
+// is a loop with a uniform trip count over register arrays indexed by the (uniform) loop counter
+// (s_set_gpr_idx, no scratch), so each f appears a handful of times in the code instead of once
+// per tree position (the unrolled form does not fit the register budget or the instruction cache
+// with a 70-instruction f).  Level q (stage s + q) combines v[m] and v[m + 2^q], m < 2^q: f when
+// the stage-(s+q) node is a left child, else g with bit base[q] + m 2^s of the path.  The same
+// operands and operations as vtree(), so the same values.
+#ifndef PL_SCL_FEX_INL
+#define PL_SCL_FEX_INL 1  // 1: vvisit_ex inlined (register arrays via s_set_gpr_idx); 0: out of line (A/B r03i:
+                          // callee register saves through scratch every pass, 4.10 vs 3.71 ms)
+#endif
+#if PL_SCL_FEX_INL
+#define PL_FEX_PASS_ATTR __forceinline__
+#else
+#define PL_FEX_PASS_ATTR __noinline__
+#endif
+template <int L, int V, int CPW>
+__device__ PL_FEX_PASS_ATTR void vvisit_ex(const float* __restrict__ llr, int64_t b0, int64_t bs, int n, int W, int per,
+                                       double lmax, unsigned char* smem, int cw_bytes, int off_A, int off_beta,
+                                       int s, int pos, int is_g, int lane) {
+    // Out of line with scalar arguments only: the pass's register arrays are allocated apart from
+    // the lane subtree's state (inlined, the two together spilled), and nothing goes through
+    // scratch but the call's own register saves, once per pass.
+    constexpr int NC = 1 << V, H = NC / 2;
+    const int ls = s - 1, h = 1 << ls, hs = 1 << s;
+    uint32_t gmask = 0u;  // level q is a g iff the stage-(s+q) node is a right child
+    int bx[V], by[V];
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+        const int st_ = s + q, pp = pos & ~((2 << st_) - 1);
+        if ((pos & ~((1 << st_) - 1)) != pp) gmask |= 1u << q;
+        bx[q] = pp;
+        by[q] = pp + h;
+    }
+    int ns = 0;  // leading f levels (uniform)
+    while (ns < V && ((gmask >> (V - 1 - ns)) & 1u) == 0u) ++ns;
+    const float* ch0 = llr + b0 * n;
+    // Register arrays as vector values: a dynamic (uniform) index lowers to s_set_gpr_idx moves,
+    // never to scratch (a plain local array in an out-of-line function goes to the stack).
+    typedef float chv __attribute__((ext_vector_type(NC)));
+    typedef double lv __attribute__((ext_vector_type(H)));
+#pragma unroll 1
+    for (int idx = lane; idx < CPW * h; idx += 64) {
+        const int c = idx >> ls, j = idx & (h - 1);
+        unsigned char* base = smem + c * cw_bytes;
+        double* A = reinterpret_cast<double*>(base + off_A);
+        const uint32_t* beta = reinterpret_cast<const uint32_t*>(base + off_beta);
+        const int co = (int)(b0 + c < bs ? c : bs - 1 - b0) * n + j;
+        chv cx, cy;  // channel elements j + m 2^s of the node's x (y: + 2^(s-1)), negated (polar_scl.py:219)
+#pragma unroll
+        for (int m = 0; m < NC; ++m) {
+            cx[m] = -1.0f * ch0[co + m * hs];
+            cy[m] = -1.0f * ch0[co + h + m * hs];
+        }
+        lv sx, sy;  // shared levels V-1 .. V-ns
+        int hh = H;
+        if (ns > 0) {
+#pragma unroll 1
+            for (int m = 0; m < H; ++m) {
+                double a, b;
+                f_ex2((double)cx[m], (double)cx[m + H], (double)cy[m], (double)cy[m + H], lmax, a, b);
+                sx[m] = a;
+                sy[m] = b;
+            }
+#pragma unroll 1
+            for (int q = V - 2; q >= V - ns; --q) {
+                hh = 1 << q;
+#pragma unroll 1
+                for (int m = 0; m < hh; ++m) {
+                    double a, b;
+                    f_ex2(sx[m], sx[m + hh], sy[m], sy[m + hh], lmax, a, b);
+                    sx[m] = a;
+                    sy[m] = b;
+                }
+            }
+        }
+#pragma unroll 1
+        for (int p = 0; p < L; ++p) {
+            const uint32_t* bp = beta + p * W;
+            lv vx, vy;
+            int q0;  // first per-path level
+            if (ns == 0) {  // the channel level is a g
+#pragma unroll 1
+                for (int m = 0; m < H; ++m) {
+                    vx[m] = g_op((double)cx[m], (double)cx[m + H], getbit(bp, bx[V - 1] + j + m * hs));
+                    vy[m] = g_op((double)cy[m], (double)cy[m + H], getbit(bp, by[V - 1] + j + m * hs));
+                }
+                q0 = V - 2;
+            } else {
+                vx = sx;
+                vy = sy;
+                q0 = V - 1 - ns;
+            }
+#pragma unroll 1
+            for (int q = q0; q >= 0; --q) {
+                const int hq = 1 << q;
+                const int ox = bx[q] + j, oy = by[q] + j;
+                if ((gmask >> q) & 1u) {
+#pragma unroll 1
+                    for (int m = 0; m < hq; ++m) {
+                        vx[m] = g_op(vx[m], vx[m + hq], getbit(bp, ox + m * hs));
+                        vy[m] = g_op(vy[m], vy[m + hq], getbit(bp, oy + m * hs));
+                    }
+                } else {
+#pragma unroll 1
+                    for (int m = 0; m < hq; ++m) {
+                        double a, b;
+                        f_ex2(vx[m], vx[m + hq], vy[m], vy[m + hq], lmax, a, b);
+                        vx[m] = a;
+                        vy[m] = b;
+                    }
+                }
+            }
+            const double x = vx[0], y = vy[0];
+            const double r = is_g ? g_op(x, y, getbit(bp, pos + j)) : f_ex(x, y, lmax);
+            A[p * per + (1 << ls) - (1 << R) + j] = r;
+        }
+    }
+}
+
 // Upper-tree node at stage s (> R), position pos: f (or g) of its input into the stage-(s-1)
 // buffers of every path of every codeword (s-1 <= SS), wave-parallel over (codeword, path,
 // element).  When the input is virtual (s = SS + 1, V stages below the channel) each lane keeps
@@ -620,6 +759,9 @@ __device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane) {
                 case 3: vvisit64<L, V, 3, FM, CPW>(t, pos, is_g, lane, wb, gmask); break;
                 default: vvisit64<L, V, 4, FM, CPW>(t, pos, is_g, lane, wb, gmask); break;
             }
+        } else if constexpr (FM == 1 && V >= 1 && PL_SCL_FEX_HOIST) {
+            vvisit_ex<L, V, CPW>(t.llr, t.b0, t.bs, t.n, t.W, t.per, t.lmax, t.smem, t.y.bytes, t.y.off_A,
+                                 t.y.off_beta, s, pos, is_g ? 1 : 0, lane);
         } else {
         // channel rows addressed from the wave's first row (uniform base, 32-bit lane offsets)
         const float* ch0 = t.llr + t.b0 * t.n;
@@ -689,13 +831,71 @@ __device__ void combine_upper(const St& t, int s, int pos, int lane) {
 // st[2^s - 1 + j] = element j of the stage-s buffer (s < R).
 constexpr int IDX(int s) { return (1 << s) - 1; }
 
-template <int s, int FM>
+// out[j] = f(in[j], in[j + h]), j < h.  Exact f (FM = 1): the path lane and its shadow hold the
+// same stage buffers, so each evaluates half of the span (the path lane j < h/2, the shadow the
+// rest, two at a time where it can: interleaved chains) and takes the other half from its partner
+// (lane ^ L) -- half the f evaluations of the lane subtree, whose values are unchanged.  MEM: the
+// input is the stage-R region in LDS, addressed per lane; otherwise registers, selected per lane.
+#ifndef PL_SCL_FEX_SPLIT
+#define PL_SCL_FEX_SPLIT 1
+#endif
+template <int h, int FM, int L, bool MEM>
+__device__ __forceinline__ void f_span(const double* in, double* out, double lmax) {
+    if constexpr (FM == 1 && h >= 2 && PL_SCL_FEX_SPLIT) {
+        constexpr int q = h / 2;
+        const int lane = threadIdx.x;
+        const bool hi = (lane & L) != 0;
+        double a[q], b[q], r[q];
+        if constexpr (MEM) {
+            const double* src = in + (hi ? q : 0);
+#pragma unroll
+            for (int j = 0; j < q; ++j) {
+                a[j] = src[j];
+                b[j] = src[j + h];
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < q; ++j) {
+                // selected as values (opaque to the compiler: a select of array addresses would put
+                // the stage buffers in scratch)
+                double a0 = in[j], a1 = in[j + q], b0 = in[j + h], b1 = in[j + q + h];
+                asm("" : "+v"(a0), "+v"(a1), "+v"(b0), "+v"(b1));
+                a[j] = hi ? a1 : a0;
+                b[j] = hi ? b1 : b0;
+            }
+        }
+        if constexpr (q == 1) {
+            r[0] = f_ex(a[0], b[0], lmax);
+        } else {
+#pragma unroll
+            for (int j = 0; j < q; j += 2) f_ex2(a[j], b[j], a[j + 1], b[j + 1], lmax, r[j], r[j + 1]);
+        }
+#pragma unroll
+        for (int j = 0; j < q; ++j) {
+            const double o = half_xchg<L>(r[j], lane);
+            out[j] = hi ? o : r[j];
+            out[j + q] = hi ? r[j] : o;
+        }
+    } else if constexpr (FM == 1 && h >= 2) {
+#pragma unroll
+        for (int j = 0; j < h; j += 2) {
+            double a, b;
+            f_ex2(in[j], in[j + h], in[j + 1], in[j + 1 + h], lmax, a, b);
+            out[j] = a;
+            out[j + 1] = b;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < h; ++j) out[j] = f_op<FM>(in[j], in[j + h], lmax);
+    }
+}
+
+template <int s, int FM, int L>
 __device__ __forceinline__ void f_down(double* st, double lmax) {
     if constexpr (s >= 1) {
         constexpr int h = 1 << (s - 1);
-#pragma unroll
-        for (int j = 0; j < h; ++j) st[IDX(s - 1) + j] = f_op<FM>(st[IDX(s) + j], st[IDX(s) + j + h], lmax);
-        f_down<s - 1, FM>(st, lmax);
+        f_span<h, FM, L, false>(st + IDX(s), st + IDX(s - 1), lmax);
+        f_down<s - 1, FM, L>(st, lmax);
     }
 }
 
@@ -708,7 +908,7 @@ __device__ __forceinline__ void load_group_fence(int j) {
 }
 
 // Leaf i (> 0) with tz = ctz(i) trailing zeros: g at stage tz+1 into stage tz, then f down.
-template <int tz, int FM>
+template <int tz, int FM, int L>
 __device__ __forceinline__ void g_step(const double* inA, double* st, uint32_t ps, int i, double lmax) {
     constexpr int h = 1 << tz;
     const int p0 = i - h;  // start of the left sibling, whose partial sums g consumes
@@ -725,7 +925,7 @@ __device__ __forceinline__ void g_step(const double* inA, double* st, uint32_t p
         st[IDX(tz) + j] = g_op(x, y, (ps >> (p0 + j)) & 1u);
         if constexpr (tz + 1 == R) load_group_fence(j);
     }
-    f_down<tz, FM>(st, lmax);
+    f_down<tz, FM, L>(st, lmax);
 }
 
 // g at stage tz+1 into stage tz for leaf i (tz = ctz(i)), without descending
@@ -747,24 +947,28 @@ __device__ __forceinline__ void g_only(const double* inA, double* st, uint32_t p
     }
 }
 
-template <int FM>
+template <int FM, int L>
 __device__ __forceinline__ void leaf_llr(const double* inA, double* st, uint32_t ps, int i, double lmax) {
     if (i == 0) {
         constexpr int h = T / 2;
+        if constexpr (FM == 1) {
+            f_span<h, FM, L, true>(inA, st + IDX(R - 1), lmax);
+        } else {
 #pragma unroll
-        for (int j = 0; j < h; ++j) {
-            st[IDX(R - 1) + j] = f_op<FM>(inA[j], inA[j + h], lmax);
-            load_group_fence(j);
+            for (int j = 0; j < h; ++j) {
+                st[IDX(R - 1) + j] = f_op<FM>(inA[j], inA[j + h], lmax);
+                load_group_fence(j);
+            }
         }
-        f_down<R - 1, FM>(st, lmax);
+        f_down<R - 1, FM, L>(st, lmax);
         return;
     }
     switch (__builtin_ctz(i)) {
-        case 0: g_step<0, FM>(inA, st, ps, i, lmax); break;
-        case 1: g_step<1, FM>(inA, st, ps, i, lmax); break;
-        case 2: g_step<2, FM>(inA, st, ps, i, lmax); break;
-        case 3: g_step<3, FM>(inA, st, ps, i, lmax); break;
-        default: g_step<R - 1, FM>(inA, st, ps, i, lmax); break;
+        case 0: g_step<0, FM, L>(inA, st, ps, i, lmax); break;
+        case 1: g_step<1, FM, L>(inA, st, ps, i, lmax); break;
+        case 2: g_step<2, FM, L>(inA, st, ps, i, lmax); break;
+        case 3: g_step<3, FM, L>(inA, st, ps, i, lmax); break;
+        default: g_step<R - 1, FM, L>(inA, st, ps, i, lmax); break;
     }
 }
 
@@ -837,7 +1041,7 @@ __device__ __forceinline__ int prune_kind(uint32_t fb, uint32_t m) {
 // Lane-level fast-SCL descent from stage s (its input st[IDX(s)] ready) at leaf position i of
 // the subtree: a rate-0 / repetition node is not descended -- returns its stage, kind 1 rate-0 /
 // 2 repetition; otherwise f down to the leaf (returns 0, st[0] = the leaf LLR).
-template <int s, int FM>
+template <int s, int FM, int L>
 __device__ __forceinline__ int descend_fast(double* st, uint32_t fz, int i, double lmax, int& kind) {
     if constexpr (s == 0) {
         return 0;
@@ -849,9 +1053,8 @@ __device__ __forceinline__ int descend_fast(double* st, uint32_t fz, int i, doub
             return s;
         }
         constexpr int h = len / 2;
-#pragma unroll
-        for (int j = 0; j < h; ++j) st[IDX(s - 1) + j] = f_op<FM>(st[IDX(s) + j], st[IDX(s) + j + h], lmax);
-        return descend_fast<s - 1, FM>(st, fz, i, lmax, kind);
+        f_span<h, FM, L, false>(st + IDX(s), st + IDX(s - 1), lmax);
+        return descend_fast<s - 1, FM, L>(st, fz, i, lmax, kind);
     }
 }
 
@@ -910,15 +1113,14 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
             if (tz + 1 == R) inA = w.A + org * t.per;  // the origin may have changed
         }
         if constexpr (!FAST) {
-            leaf_llr<FM>(inA, st, ps, i, t.lmax);
+            leaf_llr<FM, L>(inA, st, ps, i, t.lmax);
         } else {
             // the node input at stage top = R-1 (leaf 0: f of the stage-R input) or ctz(i) (g of
             // the parent's input), then the pruning descent
             int top;
             if (i == 0) {
                 constexpr int h = T / 2;
-#pragma unroll
-                for (int j = 0; j < h; ++j) st[IDX(R - 1) + j] = f_op<FM>(inA[j], inA[j + h], t.lmax);
+                f_span<h, FM, L, true>(inA, st + IDX(R - 1), t.lmax);
                 top = R - 1;
             } else {
                 top = __builtin_ctz(i);
@@ -932,9 +1134,9 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
             int kind = 0, ps_ = 0;
             switch (top) {
                 case 0: ps_ = 0; break;
-                case 1: ps_ = descend_fast<1, FM>(st, fz, i, t.lmax, kind); break;
-                case 2: ps_ = descend_fast<2, FM>(st, fz, i, t.lmax, kind); break;
-                default: ps_ = descend_fast<R - 1, FM>(st, fz, i, t.lmax, kind); break;
+                case 1: ps_ = descend_fast<1, FM, L>(st, fz, i, t.lmax, kind); break;
+                case 2: ps_ = descend_fast<2, FM, L>(st, fz, i, t.lmax, kind); break;
+                default: ps_ = descend_fast<R - 1, FM, L>(st, fz, i, t.lmax, kind); break;
             }
             if (ps_ > 0) {  // pruned node of size 2^ps_ at leaf i: its input is st[IDX(ps_)]
                 // repetition: shadow lanes evaluate the u = 1 branch (negated LLRs, dec.py:294)
