@@ -318,7 +318,7 @@ int pl_scl_decode(const pl_plan* p, const float* llr, int64_t bs, void* out, int
         pl::set_error("pl_scl_decode: unknown out_kind");
         return PL_EINVAL;
     }
-    if (ws_bytes < pl::scl_workspace_size(p, bs)) {
+    if ((ws != nullptr || ws_bytes != 0) && ws_bytes < pl::scl_workspace_size(p, bs)) {
         pl::set_error("pl_scl_decode: workspace too small");
         return PL_EINVAL;
     }

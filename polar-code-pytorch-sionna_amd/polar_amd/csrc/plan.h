@@ -47,7 +47,9 @@ bool scl_tree_eligible(const pl_plan* plan);
 // Whether some SCL kernel decodes this plan (sets the error string when not); scl_kernel.hip
 bool scl_supported(const pl_plan* plan);
 int launch_scl_tree(const pl_plan* plan, const float* llr, int64_t bs, void* out, int out_kind, double* out_pm,
-                    hipStream_t stream);
+                    void* ws, size_t ws_bytes, hipStream_t stream);
+// device scratch the subtree kernel uses (the exact-f leftmost-chain cache), 0 if none
+size_t scl_tree_workspace_size(const pl_plan* plan, int64_t bs);
 // PL_OK when the stream (NULL: the current device) is on the plan's device, else PL_EINVAL; capi.cpp
 int check_device(const pl_plan* plan, hipStream_t stream, const char* what);
 int launch_encode(const pl_plan* plan, const float* u, int64_t bs, float* cw, hipStream_t stream);

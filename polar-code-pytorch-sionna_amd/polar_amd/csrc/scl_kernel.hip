@@ -486,7 +486,7 @@ __global__ __launch_bounds__(64) void scl_decode_kernel(const float* __restrict_
 }  // namespace
 
 namespace pl {
-size_t scl_workspace_size(const pl_plan*, int64_t) { return 0; }
+size_t scl_workspace_size(const pl_plan* p, int64_t bs) { return scl_tree_workspace_size(p, bs); }
 
 // Limits of the generic kernel: its state is LDS-resident (one wave per codeword, <= 160 KiB)
 // and a fork gathers the L * n/32 partial-sum and decision words in 16 registers per lane
@@ -504,10 +504,10 @@ bool scl_supported(const pl_plan* p) {
     return true;
 }
 
-int launch_scl(const pl_plan* p, const float* llr, int64_t bs, void* out, int out_kind, double* out_pm, void*, size_t,
-               hipStream_t st) {
+int launch_scl(const pl_plan* p, const float* llr, int64_t bs, void* out, int out_kind, double* out_pm, void* ws,
+               size_t ws_bytes, hipStream_t st) {
     if (bs == 0) return PL_OK;
-    if (scl_tree_eligible(p)) return launch_scl_tree(p, llr, bs, out, out_kind, out_pm, st);
+    if (scl_tree_eligible(p)) return launch_scl_tree(p, llr, bs, out, out_kind, out_pm, ws, ws_bytes, st);
     if (!scl_supported(p)) return PL_ENOTSUP;
     const Lay y = make_layout(p->n, p->log_n, p->list_size);
     const bool fast = (p->flags & PL_PLAN_FAST_SCL) != 0;

@@ -140,6 +140,15 @@ __host__ __device__ inline Lay make_layout(int n, int S, int L, int V) {
     return y;
 }
 
+// Exact-f leftmost-chain cache (global workspace): for k = 1 .. V, the input of the leftmost
+// stage-(S-k) node, 2^(S-k) doubles at offset 2^S - 2^(S-k+1) of a codeword's slot.  Those nodes
+// are reached from the channel through f levels only, so their inputs do not depend on the path:
+// a virtual pass whose node lies below ns leading f levels reads the values of level ns from here
+// instead of evaluating ns levels of exact f (each chain value was recomputed by every pass under
+// it: 16 passes at n = 1024 for the 512 values of k = 1).
+__host__ __device__ inline int chain_size(int n, int V) { return n - (n >> V); }
+__host__ __device__ inline int chain_off(int n, int k) { return n - (n >> (k - 1)); }
+
 #if PL_SCL_FG_BITS
 // v_min_f64 without the input canonicalisation fmin() adds (a v_max_f64 per operand that is not
 // known canonical); the decoder never sees NaNs (unsupported inputs)
@@ -366,6 +375,7 @@ struct St {
     unsigned char* smem;
     Lay y;
     const float* llr;
+    double* vcache;  // exact f: this wave's leftmost-chain cache (chain_size(n, V) doubles per codeword), or null
     int64_t b0, bs;
     int n, S, W, SS, per;
     double lmax;
@@ -565,7 +575,7 @@ __device__ void vvisit64(const St& t, int pos, bool is_g, int lane, const int* w
 template <int L, int V, int CPW>
 __device__ PL_FEX_PASS_ATTR void vvisit_ex(const float* __restrict__ llr, int64_t b0, int64_t bs, int n, int W, int per,
                                        double lmax, unsigned char* smem, int cw_bytes, int off_A, int off_beta,
-                                       int s, int pos, int is_g, int lane) {
+                                       int s, int pos, int is_g, int lane, const double* __restrict__ vcache) {
     // Out of line with scalar arguments only: the pass's register arrays are allocated apart from
     // the lane subtree's state (inlined, the two together spilled), and nothing goes through
     // scratch but the call's own register saves, once per pass.
@@ -602,7 +612,17 @@ __device__ PL_FEX_PASS_ATTR void vvisit_ex(const float* __restrict__ llr, int64_
         }
         lv sx, sy;  // shared levels V-1 .. V-ns
         int hh = H;
-        if (ns > 0) {
+        if (ns > 0 && vcache != nullptr) {  // level ns of the leftmost chain: element j + m 2^s (x), + h (y)
+            hh = NC >> ns;
+            const double* cb = vcache + c * chain_size(n, V) + chain_off(n, ns) + j;
+#pragma unroll
+            for (int m = 0; m < H; ++m) {
+                if (m < hh) {
+                    sx[m] = cb[m * hs];
+                    sy[m] = cb[h + m * hs];
+                }
+            }
+        } else if (ns > 0) {
 #pragma unroll 1
             for (int m = 0; m < H; ++m) {
                 double a, b;
@@ -761,7 +781,7 @@ __device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane) {
             }
         } else if constexpr (FM == 1 && V >= 1 && PL_SCL_FEX_HOIST) {
             vvisit_ex<L, V, CPW>(t.llr, t.b0, t.bs, t.n, t.W, t.per, t.lmax, t.smem, t.y.bytes, t.y.off_A,
-                                 t.y.off_beta, s, pos, is_g ? 1 : 0, lane);
+                                 t.y.off_beta, s, pos, is_g ? 1 : 0, lane, t.vcache);
         } else {
         // channel rows addressed from the wave's first row (uniform base, 32-bit lane offsets)
         const float* ch0 = t.llr + t.b0 * t.n;
@@ -1277,11 +1297,11 @@ __device__ __forceinline__ int node_kind(const uint32_t* __restrict__ fw, int s,
 
 // Re-point the upper-tree state of every path to its origin path org_s[]: partial-sum words
 // before i0 and the stage owners.
-template <int L, int CPW>
+template <int L, int V, int CPW>
 __device__ void repoint(const St& t, int i0, int lane) {
     constexpr int LL = ilog2(L);
 #if PL_SCL_REPOINT_VEC
-    if (t.W >= 4) {
+    if (V >= 2 || t.W >= 4) {  // V >= 2: n >= 128, so W >= 4 (the word loop below is not compiled in)
         // two lanes per (codeword, path) pair (CPW * L = 32): one origin load each, the pair's
         // partial-sum row in 16-byte quads (words past i0 are copied too: they belong to leaves
         // not decided yet and are overwritten before anything reads them) and its 16-byte
@@ -1309,6 +1329,7 @@ __device__ void repoint(const St& t, int i0, int lane) {
         return;
     }
 #endif
+    if constexpr (PL_SCL_REPOINT_VEC && V >= 2) return;
     const int W = t.W, w_lim = (i0 + 31) >> 5;
     // CPW * L = 32 (codeword, path) pairs per wave, <= 32 words each (n <= 1024)
     constexpr int RB = 32 * 32 / 64;
@@ -1375,7 +1396,7 @@ __device__ void upper_prune(const St& t, int s, int pos, int kind, double& pm, i
     pm = npm;
     if (gl < L) w.org_s[gl] = par;
     __syncthreads();
-    repoint<L, CPW>(t, pos, lane);
+    repoint<L, V, CPW>(t, pos, lane);
     if (gl < L && bit) {
         const int b = pos + (1 << s) - T;
         w.beta[gl * t.W + (b >> 5)] |= ((1u << T) - 1u) << (b & 31);
@@ -1392,7 +1413,8 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
                                                       int out_kind, double* __restrict__ out_pm,
                                                       const uint32_t* __restrict__ frozen_words,
                                                       const int32_t* __restrict__ info_pos, int n, int S, int k,
-                                                      double lmax, int crc_deg, uint32_t crc_g) {
+                                                      double lmax, int crc_deg, uint32_t crc_g,
+                                                      double* __restrict__ vcache) {
     constexpr int GW = 2 * L, CPW = 64 / GW, LL = ilog2(L);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x;
@@ -1408,6 +1430,7 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
     t.SS = t.y.SS;
     t.per = t.y.per;
     t.lmax = lmax;
+    t.vcache = (FM == 1 && V >= 1 && vcache != nullptr) ? vcache + t.b0 * chain_size(n, V) : nullptr;
     const int W = t.W, LW = ilog2(W);
     const int gl = lane & (GW - 1), my_c = lane / GW;
     const Cw mine = t.cw(my_c);
@@ -1423,6 +1446,43 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
             w.A[i % T] = (double)(-1.0f * w.ch[i % T]);
         }
     __syncthreads();
+
+    if constexpr (FM == 1 && V >= 1) {
+        if (t.vcache != nullptr) {  // fill the leftmost chain, level by level (wave-parallel, pairs of f)
+            const int cs = chain_size(n, V);
+#pragma unroll 1
+            for (int k = 1; k <= V; ++k) {
+                const int sz = n >> k, lsz = S - k;
+                const double* prev = t.vcache + (k > 1 ? chain_off(n, k - 1) : 0);
+                double* cur = t.vcache + chain_off(n, k);
+#pragma unroll 1
+                for (int i0 = lane; i0 < CPW * sz; i0 += 128) {
+                    double a[2], b[2], r[2];
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const int idx = min(i0 + 64 * u, CPW * sz - 1);  // a clamped duplicate is recomputed, not stored
+                        const int c = idx >> lsz, i = idx & (sz - 1);
+                        if (k == 1) {
+                            const float* ch = t.cw(c).ch;
+                            a[u] = (double)(-1.0f * ch[i]);
+                            b[u] = (double)(-1.0f * ch[i + sz]);
+                        } else {
+                            a[u] = prev[c * cs + i];
+                            b[u] = prev[c * cs + i + sz];
+                        }
+                    }
+                    f_ex2(a[0], b[0], a[1], b[1], t.lmax, r[0], r[1]);
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        const int idx = i0 + 64 * u;
+                        if (idx < CPW * sz) cur[(idx >> lsz) * cs + (idx & (sz - 1))] = r[u];
+                    }
+                }
+                __threadfence_block();
+                __syncthreads();
+            }
+        }
+    }
 
     double pm = gl == 0 || gl == L ? 0.0 : lmax;  // :192-194 ([0, 30 x (L-1)] per half)
     const int nsub = n >> R;
@@ -1463,7 +1523,7 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
             // subtree's partial sums: partial-sum words before i0 and stage owners R..SS
             if (gl < L) mine.org_s[gl] = org;
             __syncthreads();
-            if (!PL_SCL_DIAG_NO_REPOINT) repoint<L, CPW>(t, i0, lane);
+            if (!PL_SCL_DIAG_NO_REPOINT) repoint<L, V, CPW>(t, i0, lane);
             const int w_i = i0 >> 5, off = i0 & 31;
             if (gl < L) {
                 uint32_t* bw = mine.beta + gl * W + w_i;
@@ -1620,8 +1680,19 @@ bool scl_tree_eligible(const pl_plan* p) {
     return p->list_size >= 2 && p->list_size <= 32 && p->log_n >= 5 && p->log_n <= 10;
 }
 
+// Workspace: the exact-f kernels' leftmost-chain cache, one slot per codeword of every launched
+// wave (a tail wave's clamped codewords get their own slots).
+size_t scl_tree_workspace_size(const pl_plan* p, int64_t bs) {
+    if (!scl_tree_eligible(p) || p->f_mode != PL_F_EXACT || bs <= 0) return 0;
+    const int V = pick_v(p->log_n);
+    if (V < 1) return 0;
+    const int cpw = 32 / p->list_size;
+    const int64_t slots = (bs + cpw - 1) / cpw * cpw;
+    return (size_t)slots * (size_t)chain_size(p->n, V) * sizeof(double);
+}
+
 int launch_scl_tree(const pl_plan* p, const float* llr, int64_t bs, void* out, int out_kind, double* out_pm,
-                    hipStream_t st) {
+                    void* ws, size_t ws_bytes, hipStream_t st) {
     if (bs == 0) return PL_OK;
     if (bs > 0x7fffffffLL) {
         set_error("SCL decode: batch too large for one launch");
@@ -1658,8 +1729,10 @@ int launch_scl_tree(const pl_plan* p, const float* llr, int64_t bs, void* out, i
     uint32_t cg = p->crc_g;
     const uint32_t* fw = p->d_frozen_words;
     const int32_t* ip = p->d_info_pos;
+    double* vc = ws_bytes >= scl_tree_workspace_size(p, bs) && scl_tree_workspace_size(p, bs) > 0
+                     ? static_cast<double*>(ws) : nullptr;
     void* args[] = {(void*)&llr, (void*)&bs, (void*)&out, (void*)&out_kind, (void*)&out_pm, (void*)&fw,
-                    (void*)&ip, (void*)&n, (void*)&S, (void*)&k, (void*)&lmax, (void*)&cdeg, (void*)&cg};
+                    (void*)&ip, (void*)&n, (void*)&S, (void*)&k, (void*)&lmax, (void*)&cdeg, (void*)&cg, (void*)&vc};
     const int64_t blocks = (bs + cpw - 1) / cpw;
     hipError_t e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(64), args, lds, st);
     if (e != hipSuccess) return check_hip(e, "SCL decode launch (subtree kernel)");

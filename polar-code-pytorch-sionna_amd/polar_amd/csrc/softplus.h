@@ -135,7 +135,88 @@ __device__ __forceinline__ double pm_log(double y) {  // y >= 1, finite
     return fma(de, kLn2Hi, fma(de, kLn2Lo, lm));
 }
 
+// Economised forms (PL_SP_FORM 1: Horner, 2: Estrin), the same three roundings -- e = exp(z),
+// y = 1 + e, log(y):
+//   exp(r) = 1 + r + r^2 P(r), P the degree-9 Chebyshev economisation of (e^r - 1 - r)/r^2 on
+//            |r| <= ln2/2 (tail < 1.1e-16, times r^2 <= 0.12; tools/cheb_coeffs.py);
+//   log m  = 2s + s z RL(z), z = s^2 <= 0.0295, RL the degree-6 economisation of
+//            sum 2/(2i+1) z^(i-1) (tail < 3.1e-16, times s z <= 0.005);
+//   s = f / (2 + f): a reciprocal, two Newton steps and a residual correction (denominator in
+//   [1.41, 2.83]) instead of the scaled IEEE division sequence.
+// 7 fewer FMAs and a shorter division than the Taylor forms above, same accuracy class (~1 ulp).
+#ifndef PL_SP_FORM
+#define PL_SP_FORM 2  // A/B r03l: 0.990 vs 1.000 ms (min-sum), 1.050 vs 1.113 ms (min-sum fast-SCL)
+#endif
+__device__ constexpr double kSpP[10] = {
+    0.5000000000000001, 0.1666666666666667, 0.04166666666662413, 0.008333333333326136,
+    0.001388888891721154, 0.00019841269874817515, 2.4801521299750923e-05, 2.75572554044176e-06,
+    2.7620086491464514e-07, 2.5105215165649368e-08};
+__device__ constexpr double kSpRL[7] = {
+    0.666666666666667, 0.39999999999898955, 0.2857142862619623, 0.22222211102348335,
+    0.18182891280109284, 0.15331655663402047, 0.14617206088074544};
+template <bool ESTRIN>
+__device__ __forceinline__ double pm_exp_e(double z) {
+    constexpr double kLog2e = 1.4426950408889634;
+    constexpr double kLn2Hi = 0x1.62e42fefa39efp-1, kLn2Lo = 0x1.abc9e3b39803fp-56;
+    const double k = __builtin_rint(z * kLog2e);
+    double r = fma(-k, kLn2Hi, z);
+    r = fma(-k, kLn2Lo, r);
+    const double r2 = r * r;
+    double P;
+    if constexpr (ESTRIN) {
+        const double a = fma(kSpP[9], r, kSpP[8]), b = fma(kSpP[7], r, kSpP[6]), c = fma(kSpP[5], r, kSpP[4]);
+        const double d = fma(kSpP[3], r, kSpP[2]), e = fma(kSpP[1], r, kSpP[0]);
+        const double r4 = r2 * r2;
+        const double ab = fma(a, r2, b), cd = fma(c, r2, d);
+        P = fma(fma(ab, r4, cd), r2, e);
+    } else {
+        P = kSpP[9];
+#pragma unroll
+        for (int i = 8; i >= 0; --i) P = fma(P, r, kSpP[i]);
+    }
+    return ldexp(fma(r2, P, r) + 1.0, (int)k);
+}
+template <bool ESTRIN>
+__device__ __forceinline__ double pm_log_e(double y) {  // y >= 1, finite
+    constexpr double kLn2Hi = 0x1.62e42fefa39efp-1, kLn2Lo = 0x1.abc9e3b39803fp-56;
+    double m = __builtin_amdgcn_frexp_mant(y);  // [0.5, 1)
+    int e = __builtin_amdgcn_frexp_exp(y);
+    if (m < 0.70710678118654752) {
+        m = m + m;
+        e -= 1;
+    }
+    const double f = m - 1.0;  // exact (Sterbenz)
+    const double den = 2.0 + f;
+    double rc = __builtin_amdgcn_rcp(den);
+    double t = fma(-den, rc, 1.0);
+    rc = fma(rc, t, rc);
+    t = fma(-den, rc, 1.0);
+    rc = fma(rc, t, rc);
+    const double q = f * rc;
+    const double s = fma(rc, fma(-den, q, f), q);
+    const double z = s * s;
+    double R;
+    if constexpr (ESTRIN) {
+        const double p01 = fma(kSpRL[1], z, kSpRL[0]), p23 = fma(kSpRL[3], z, kSpRL[2]);
+        const double p45 = fma(kSpRL[5], z, kSpRL[4]);
+        const double z2 = z * z, z4 = z2 * z2;
+        R = fma(fma(kSpRL[6], z2, p45), z4, fma(p23, z2, p01));
+    } else {
+        R = kSpRL[6];
+#pragma unroll
+        for (int i = 5; i >= 0; --i) R = fma(R, z, kSpRL[i]);
+    }
+    const double lm = fma(s * z, R, s + s);  // log m = 2s + s z R(z)
+    const double de = (double)e;
+    return fma(de, kLn2Hi, fma(de, kLn2Lo, lm));
+}
+#if PL_SP_FORM == 0
 __device__ __forceinline__ double softplus_pm(double z) { return pm_log(1.0 + pm_exp(z)); }
+#else
+__device__ __forceinline__ double softplus_pm(double z) {
+    return pm_log_e<PL_SP_FORM == 2>(1.0 + pm_exp_e<PL_SP_FORM == 2>(z));
+}
+#endif
 
 // The exact boxplus of the my_sn list decoder (my_sn/fec/polar/dec.py:330-339, float64),
 //   f = log(1 + e^(x+y)) - log(e^x + e^y)

@@ -46,10 +46,19 @@ def _compile_asm(src_path, extra, workdir):
     return open(out).read()
 
 
+_SCL_ASM = {}
+
+
+def _scl_l8_asm():
+    if "asm" not in _SCL_ASM:
+        src = os.path.join(_build.CSRC, "scl_tree_kernel.hip")
+        with tempfile.TemporaryDirectory() as td:
+            _SCL_ASM["asm"] = _compile_asm(src, ["-DPL_SCL_TREE_L=8"], td)
+    return _SCL_ASM["asm"]
+
+
 def test_scl_bench_kernel_has_no_spills_or_scratch():
-    src = os.path.join(_build.CSRC, "scl_tree_kernel.hip")
-    with tempfile.TemporaryDirectory() as td:
-        asm = _compile_asm(src, ["-DPL_SCL_TREE_L=8"], td)
+    asm = _scl_l8_asm()
     # scl_tree_kernel<L = 8, V = 4, f_mode = 0 (min-sum), FAST = false>: the kernel bench.py --decoder scl runs
     meta = _kernel_meta(asm, lambda n: "scl_tree_kernelILi8ELi4ELi0ELb0E" in n)
     assert len(meta) == 1, list(meta)
@@ -57,6 +66,21 @@ def test_scl_bench_kernel_has_no_spills_or_scratch():
     assert m["vgpr_spill_count"] == 0, m
     assert m["private_segment_fixed_size"] == 0, m
     assert m["vgpr_count"] <= 256, m  # amdgpu_waves_per_eu(2)
+
+
+def test_scl_exact_f_kernels_have_no_spills():
+    """The exact-f (FM = 1) subtree kernels at n = 512 / 1024 (V = 3, 4) -- my_sn SCL_Dec's default
+    (with and without fast-SCL) and Polar5GDecoder's list decoder: no VGPR spills, and no scratch
+    beyond the 16-byte frame of the out-of-line virtual-stage term (vterm) the fast kernels call."""
+    asm = _scl_l8_asm()
+    for v in (3, 4):
+        for fast in ("0", "1"):
+            meta = _kernel_meta(asm, lambda n: f"scl_tree_kernelILi8ELi{v}ELi1ELb{fast}E" in n)
+            assert len(meta) == 1, (v, fast, list(meta))
+            (m,) = meta.values()
+            assert m["vgpr_spill_count"] == 0, (v, fast, m)
+            assert m["private_segment_fixed_size"] <= (16 if fast == "1" else 0), (v, fast, m)
+            assert m["vgpr_count"] <= 256, (v, fast, m)
 
 
 def test_sc_bench_kernel_fits_four_waves_per_simd():

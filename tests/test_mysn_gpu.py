@@ -227,3 +227,39 @@ def test_scl_n2048_module_and_limits(pa):
     assert np.abs(dec.msg_pm - wpm).max() < 1e-9
     with pytest.raises(ValueError, match="list_size"):
         pa.SCL_Dec(fp, n, list_size=32)
+
+
+@pytest.mark.parametrize("n,k,fast", [(1024, 512, True), (1024, 512, False), (512, 256, True), (256, 128, True)])
+def test_exact_scl_chain_cache_is_transparent(pa, n, k, fast):
+    """The exact-f subtree kernel's leftmost-chain cache (the pl_scl_decode workspace) changes no
+    bit and no metric: decoding with the workspace equals decoding with NULL (the chain recomputed
+    in every virtual pass), including a tail wave (bs not a multiple of the codewords per wave)."""
+    import ctypes
+
+    from polar_amd import _lib, ops
+    fp = pa.reference_frozen_pos(k, n).numpy()
+    flags = _lib.PL_PLAN_FAST_SCL if fast else 0
+    plan = _lib.Plan(n, pa.frozen_mask(fp, n), 8, _lib.PL_F_EXACT, flags=flags)
+    bs = 67
+    assert int(_lib.lib().pl_scl_workspace_size(plan.handle, bs)) == 68 * (n - (n >> plan_v(n))) * 8
+    g = torch.Generator(device="cuda").manual_seed(n + fast)
+    llr = (torch.randn((bs, n), device="cuda", generator=g) * 2.0 + 0.8).contiguous()
+    bits, pm = ops.scl_decode(plan, llr, return_pm=True)
+    out = torch.empty((bs, k), device="cuda")
+    pm0 = torch.empty((bs, 16), device="cuda", dtype=torch.float64)
+    L = _lib.lib()
+    _lib.check(L.pl_scl_decode(plan.handle, ctypes.c_void_p(llr.data_ptr()), bs, ctypes.c_void_p(out.data_ptr()),
+                               _lib.PL_OUT_F32, ctypes.c_void_p(pm0.data_ptr()), None, 0,
+                               _lib.current_stream_ptr(llr.device)), "pl_scl_decode")
+    torch.cuda.synchronize()
+    assert torch.equal(bits, out)
+    assert torch.equal(pm, pm0)
+
+
+def plan_v(n):
+    """Virtual stages of the subtree kernel at code length n (scl_tree_kernel.hip pick_v)."""
+    S = n.bit_length() - 1
+    v = min(S - 1 - 4, 4)
+    if v == 4 and S != 10:
+        v = 3
+    return max(v, 0)

@@ -60,14 +60,19 @@ def time_all(n=1024, k=512, bs=8192, reps=5, rounds=2):
         flags = int(os.environ.get("SCL_FLAGS", "0"))  # e.g. 4 = PL_PLAN_FAST_SCL
         fmode = int(os.environ.get("SCL_FMODE", "0"))
         assert L.pl_plan_create(ctypes.byref(h), n, mask.ctypes.data_as(ctypes.c_void_p), 8, fmode, 30.0, flags) == 0
-        handles.append((name, L, h))
+        handles.append((name, L, h, True))
+        if os.environ.get("SCL_WS_AB") == "1":  # the same library without its workspace (exact-f chain cache off)
+            handles.append((name + "-nows", L, h, False))
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     for rnd in range(rounds):
-        for name, L, h in handles:
+        for name, L, h, use_ws in handles:
             out = torch.empty((bs, k), device="cuda")
             pm = torch.empty((bs, 16), device="cuda", dtype=torch.float64)
+            wsb = int(L.pl_scl_workspace_size(h, bs)) if use_ws else 0
+            ws = torch.empty((max(wsb, 1),), dtype=torch.uint8, device="cuda")
             call = lambda: L.pl_scl_decode(h, ctypes.c_void_p(llr.data_ptr()), bs, ctypes.c_void_p(out.data_ptr()),  # noqa
-                                           0, ctypes.c_void_p(pm.data_ptr()), None, 0, stream)
+                                           0, ctypes.c_void_p(pm.data_ptr()),
+                                           ctypes.c_void_p(ws.data_ptr() if wsb else 0), wsb, stream)
             assert call() == 0, L.pl_last_error_string()
             torch.cuda.synchronize()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
