@@ -36,6 +36,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../../include/polar_mi355x.h"
 #include "plan.h"
 #include "softplus.h"
@@ -563,6 +565,9 @@ __device__ void vvisit64(const St& t, int pos, bool is_g, int lane, const int* w
 // with a 70-instruction f).  Level q (stage s + q) combines v[m] and v[m + 2^q], m < 2^q: f when
 // the stage-(s+q) node is a left child, else g with bit base[q] + m 2^s of the path.  The same
 // operands and operations as vtree(), so the same values.
+#ifndef PL_SCL_FEX_COMBO
+#define PL_SCL_FEX_COMBO 1  // 1: the f level after the first per-path g from its four path-independent outcomes
+#endif
 #ifndef PL_SCL_FEX_INL
 #define PL_SCL_FEX_INL 1  // 1: vvisit_ex inlined (register arrays via s_set_gpr_idx); 0: out of line (A/B r03i:
                           // callee register saves through scratch every pass, 4.10 vs 3.71 ms)
@@ -595,8 +600,14 @@ __device__ PL_FEX_PASS_ATTR void vvisit_ex(const float* __restrict__ llr, int64_
     const float* ch0 = llr + b0 * n;
     // Register arrays as vector values: a dynamic (uniform) index lowers to s_set_gpr_idx moves,
     // never to scratch (a plain local array in an out-of-line function goes to the stack).
-    typedef float chv __attribute__((ext_vector_type(NC)));
     typedef double lv __attribute__((ext_vector_type(H)));
+    const int q1 = V - 1 - ns, h1 = 1 << (q1 > 0 ? q1 : 0), h2 = h1 >> 1;
+    // First per-path level q1 (a g) followed by an f: each input of that f is one of two
+    // path-independent sums (g with u = 0 or 1), so its four outcomes per element are computed
+    // once and a path selects one by its two partial-sum bits -- 4 h2 f per side instead of h2 per
+    // path (8 paths).  Same operands and operations as the per-path evaluation.
+    const bool combo = PL_SCL_FEX_COMBO && ns < V && q1 >= 1 && ((gmask >> (q1 - 1)) & 1u) == 0u;
+    typedef double wv __attribute__((ext_vector_type(NC)));
 #pragma unroll 1
     for (int idx = lane; idx < CPW * h; idx += 64) {
         const int c = idx >> ls, j = idx & (h - 1);
@@ -604,42 +615,63 @@ __device__ PL_FEX_PASS_ATTR void vvisit_ex(const float* __restrict__ llr, int64_
         double* A = reinterpret_cast<double*>(base + off_A);
         const uint32_t* beta = reinterpret_cast<const uint32_t*>(base + off_beta);
         const int co = (int)(b0 + c < bs ? c : bs - 1 - b0) * n + j;
-        chv cx, cy;  // channel elements j + m 2^s of the node's x (y: + 2^(s-1)), negated (polar_scl.py:219)
+        // One register block per side holds what the path loop reads: the channel elements
+        // j + m 2^s (x; y: + 2^(s-1)) as doubles when the channel level is per path (ns = 0), the
+        // shared level-ns values (ns > 0), or the four-outcome table w[m + (2 b1 + b2) h2] (combo).
+        wv wx, wy;
+        int hh = NC;
+        if (ns == 0 || vcache == nullptr) {
 #pragma unroll
-        for (int m = 0; m < NC; ++m) {
-            cx[m] = -1.0f * ch0[co + m * hs];
-            cy[m] = -1.0f * ch0[co + h + m * hs];
+            for (int m = 0; m < NC; ++m) {
+                wx[m] = (double)(-1.0f * ch0[co + m * hs]);  // negated (polar_scl.py:219)
+                wy[m] = (double)(-1.0f * ch0[co + h + m * hs]);
+            }
         }
-        lv sx, sy;  // shared levels V-1 .. V-ns
-        int hh = H;
         if (ns > 0 && vcache != nullptr) {  // level ns of the leftmost chain: element j + m 2^s (x), + h (y)
             hh = NC >> ns;
             const double* cb = vcache + c * chain_size(n, V) + chain_off(n, ns) + j;
 #pragma unroll
             for (int m = 0; m < H; ++m) {
                 if (m < hh) {
-                    sx[m] = cb[m * hs];
-                    sy[m] = cb[h + m * hs];
+                    wx[m] = cb[m * hs];
+                    wy[m] = cb[h + m * hs];
                 }
             }
-        } else if (ns > 0) {
+        } else if (ns > 0) {  // shared levels V-1 .. V-ns evaluated here
 #pragma unroll 1
-            for (int m = 0; m < H; ++m) {
-                double a, b;
-                f_ex2((double)cx[m], (double)cx[m + H], (double)cy[m], (double)cy[m + H], lmax, a, b);
-                sx[m] = a;
-                sy[m] = b;
-            }
-#pragma unroll 1
-            for (int q = V - 2; q >= V - ns; --q) {
+            for (int q = V - 1; q >= V - ns; --q) {
                 hh = 1 << q;
 #pragma unroll 1
                 for (int m = 0; m < hh; ++m) {
                     double a, b;
-                    f_ex2(sx[m], sx[m + hh], sy[m], sy[m + hh], lmax, a, b);
-                    sx[m] = a;
-                    sy[m] = b;
+                    f_ex2(wx[m], wx[m + hh], wy[m], wy[m + hh], lmax, a, b);
+                    wx[m] = a;
+                    wy[m] = b;
                 }
+            }
+        }
+        if (combo) {  // in place: block m reads and writes exactly the indices m + k h2, k < 4
+#pragma unroll 1
+            for (int m = 0; m < h2; ++m) {
+                const double xa = wx[m], xb = wx[m + h1], xc_ = wx[m + h2], xd = wx[m + h2 + h1];
+                const double ya = wy[m], yb = wy[m + h1], yc_ = wy[m + h2], yd = wy[m + h2 + h1];
+                const double gx0 = g_op(xa, xb, 0u), gx1 = g_op(xa, xb, 1u);
+                const double hx0 = g_op(xc_, xd, 0u), hx1 = g_op(xc_, xd, 1u);
+                const double gy0 = g_op(ya, yb, 0u), gy1 = g_op(ya, yb, 1u);
+                const double hy0 = g_op(yc_, yd, 0u), hy1 = g_op(yc_, yd, 1u);
+                double r0, r1, r2, r3, t0, t1, t2, t3;
+                f_ex2(gx0, hx0, gx0, hx1, lmax, r0, r1);
+                f_ex2(gx1, hx0, gx1, hx1, lmax, r2, r3);
+                f_ex2(gy0, hy0, gy0, hy1, lmax, t0, t1);
+                f_ex2(gy1, hy0, gy1, hy1, lmax, t2, t3);
+                wx[m] = r0;
+                wx[m + h2] = r1;
+                wx[m + 2 * h2] = r2;
+                wx[m + 3 * h2] = r3;
+                wy[m] = t0;
+                wy[m + h2] = t1;
+                wy[m + 2 * h2] = t2;
+                wy[m + 3 * h2] = t3;
             }
         }
 #pragma unroll 1
@@ -647,16 +679,40 @@ __device__ PL_FEX_PASS_ATTR void vvisit_ex(const float* __restrict__ llr, int64_
             const uint32_t* bp = beta + p * W;
             lv vx, vy;
             int q0;  // first per-path level
-            if (ns == 0) {  // the channel level is a g
+            if (combo) {
+                const int ox = bx[q1] + j, oy = by[q1] + j;
+                // static register indices per table size (h2 = 1, 2, 4: a uniform branch)
+                auto pick = [&](auto H2c) {
+                    constexpr int H2 = decltype(H2c)::value;
+#pragma unroll
+                    for (int m = 0; m < H2; ++m) {
+                        const uint32_t bx1 = getbit(bp, ox + m * hs), bx2 = getbit(bp, ox + (m + H2) * hs);
+                        const uint32_t by1 = getbit(bp, oy + m * hs), by2 = getbit(bp, oy + (m + H2) * hs);
+                        vx[m] = bx1 ? (bx2 ? wx[m + 3 * H2] : wx[m + 2 * H2]) : (bx2 ? wx[m + H2] : wx[m]);
+                        vy[m] = by1 ? (by2 ? wy[m + 3 * H2] : wy[m + 2 * H2]) : (by2 ? wy[m + H2] : wy[m]);
+                    }
+                };
+                if constexpr (H >= 8) {
+                    if (h2 == 4) pick(std::integral_constant<int, (H >= 8 ? 4 : 1)>{});
+                }
+                if constexpr (H >= 4) {
+                    if (h2 == 2) pick(std::integral_constant<int, (H >= 4 ? 2 : 1)>{});
+                }
+                if (h2 == 1) pick(std::integral_constant<int, 1>{});
+                q0 = q1 - 2;
+            } else if (ns == 0) {  // the channel level is a g
 #pragma unroll 1
                 for (int m = 0; m < H; ++m) {
-                    vx[m] = g_op((double)cx[m], (double)cx[m + H], getbit(bp, bx[V - 1] + j + m * hs));
-                    vy[m] = g_op((double)cy[m], (double)cy[m + H], getbit(bp, by[V - 1] + j + m * hs));
+                    vx[m] = g_op(wx[m], wx[m + H], getbit(bp, bx[V - 1] + j + m * hs));
+                    vy[m] = g_op(wy[m], wy[m + H], getbit(bp, by[V - 1] + j + m * hs));
                 }
                 q0 = V - 2;
             } else {
-                vx = sx;
-                vy = sy;
+#pragma unroll 1
+                for (int m = 0; m < hh; ++m) {
+                    vx[m] = wx[m];
+                    vy[m] = wy[m];
+                }
                 q0 = V - 1 - ns;
             }
 #pragma unroll 1
