@@ -11,7 +11,7 @@
 // with them evaluated in fp64 and rounded once it matches the reference on every row).
 //
 // exp_cr / log_cr evaluate in fp64 over the range f uses and round once to fp32; their fp64
-// error (< 2^-46 relative) leaves a wrong fp32 rounding only for arguments within 2^-22 ulp of a
+// error (< 2^-50 relative) leaves a wrong fp32 rounding only for arguments within 2^-26 ulp of a
 // rounding boundary.  Range: exp_cr for |x| <= 87 (normal fp32 results), log_cr for finite x > 0.
 #pragma once
 #ifndef __HIPCC_RTC__
@@ -20,8 +20,21 @@
 
 namespace plx {
 
-// exp(x) for fp32 x, |x| <= 87: x = k ln2 + r (|r| <= ln2/2, two-part ln2), Taylor polynomial of
-// degree 11 in fp64 (truncation < 7e-15 relative), rounded to fp32, then scaled by 2^k exactly.
+// Polynomials: Chebyshev economisations (tools/cheb_coeffs.py) of the Taylor series -- e^r on
+// |r| <= ln2/2 at degree 10 (tail < 2.2e-16, was Taylor degree 11: 7e-15) and the atanh series
+// sum 2/(2i+1) z^(i-1) on z <= 0.0295 at degree 5 (tail < 5e-14, times s z <= 0.005: below 3e-16
+// relative to log m, as the Taylor degree 8 it replaces).  Checked on the host against expl/logl
+// rounded to fp32: 0 of 5e7 exp and 1 of 5e7 log arguments misrounded, the same as the Taylor forms.
+__device__ constexpr double kExpC[11] = {
+    1.0, 1.0000000000000067, 0.5000000000000019, 0.16666666666554325, 0.041666666666487974,
+    0.008333333385695266, 0.001388888895234707, 0.00019841170236135905, 2.480148544815057e-05,
+    2.7640194893802356e-06, 2.763265216957956e-07};
+__device__ constexpr double kLogC[6] = {
+    0.6666666666666206, 0.40000000011263015, 0.2857142412272895, 0.22222863785496652,
+    0.18140134518808063, 0.16622633991749486};
+
+// exp(x) for fp32 x, |x| <= 87: x = k ln2 + r (|r| <= ln2/2, two-part ln2), degree-10 polynomial
+// in fp64, rounded to fp32, then scaled by 2^k exactly.
 __device__ __forceinline__ float exp_cr(float xf) {
     const double x = (double)xf;
     constexpr double kLog2e = 1.4426950408889634;
@@ -29,24 +42,16 @@ __device__ __forceinline__ float exp_cr(float xf) {
     const double k = __builtin_rint(x * kLog2e);
     double r = __builtin_fma(-k, kLn2Hi, x);
     r = __builtin_fma(-k, kLn2Lo, r);
-    double p = 2.505210838544172e-08;  // 1/11!
-    p = __builtin_fma(p, r, 2.755731922398589e-07);
-    p = __builtin_fma(p, r, 2.7557319223985893e-06);
-    p = __builtin_fma(p, r, 2.48015873015873e-05);
-    p = __builtin_fma(p, r, 0.0001984126984126984);
-    p = __builtin_fma(p, r, 0.001388888888888889);
-    p = __builtin_fma(p, r, 0.008333333333333333);
-    p = __builtin_fma(p, r, 0.041666666666666664);
-    p = __builtin_fma(p, r, 0.16666666666666666);
-    p = __builtin_fma(p, r, 0.5);
-    p = __builtin_fma(p, r, 1.0);
-    p = __builtin_fma(p, r, 1.0);
+    double p = kExpC[10];
+#pragma unroll
+    for (int i = 9; i >= 0; --i) p = __builtin_fma(p, r, kExpC[i]);
     // p in [0.70, 1.42]: rounding p and scaling by 2^k (|k| <= 126, a normal result) is one rounding
     return __builtin_ldexpf((float)p, (int)k);
 }
 
 // log(x) for finite fp32 x > 0: x = 2^e m, m in [sqrt(1/2), sqrt(2)), log m = 2 atanh(s) with
-// s = (m - 1) / (m + 1), |s| < 0.1716, series through s^19 (truncation < 3e-16 relative), in fp64.
+// s = (m - 1) / (m + 1), |s| < 0.1716, in fp64; the quotient from a reciprocal with two Newton
+// steps and a residual correction (denominator in [1.41, 2.83]).
 __device__ __forceinline__ float log_cr(float xf) {
     constexpr double kLn2Hi = 0x1.62e42fefa39efp-1, kLn2Lo = 0x1.abc9e3b39803fp-56;
     double m = __builtin_amdgcn_frexp_mant((double)xf);  // [0.5, 1)
@@ -56,17 +61,18 @@ __device__ __forceinline__ float log_cr(float xf) {
         e -= 1;
     }
     const double f = m - 1.0;  // exact
-    const double s = f / (2.0 + f);
+    const double den = 2.0 + f;
+    double rc = __builtin_amdgcn_rcp(den);
+    double t = __builtin_fma(-den, rc, 1.0);
+    rc = __builtin_fma(rc, t, rc);
+    t = __builtin_fma(-den, rc, 1.0);
+    rc = __builtin_fma(rc, t, rc);
+    const double q = f * rc;
+    const double s = __builtin_fma(rc, __builtin_fma(-den, q, f), q);
     const double z = s * s;
-    double R = 2.0 / 19.0;  // sum_{i>=1} 2/(2i+1) z^(i-1), i = 1 .. 9
-    R = __builtin_fma(R, z, 2.0 / 17.0);
-    R = __builtin_fma(R, z, 2.0 / 15.0);
-    R = __builtin_fma(R, z, 2.0 / 13.0);
-    R = __builtin_fma(R, z, 2.0 / 11.0);
-    R = __builtin_fma(R, z, 2.0 / 9.0);
-    R = __builtin_fma(R, z, 2.0 / 7.0);
-    R = __builtin_fma(R, z, 2.0 / 5.0);
-    R = __builtin_fma(R, z, 2.0 / 3.0);
+    double R = kLogC[5];
+#pragma unroll
+    for (int i = 4; i >= 0; --i) R = __builtin_fma(R, z, kLogC[i]);
     const double lm = __builtin_fma(s * z, R, s + s);  // log m = 2s + s z R(z)
     const double de = (double)e;
     return (float)__builtin_fma(de, kLn2Hi, __builtin_fma(de, kLn2Lo, lm));

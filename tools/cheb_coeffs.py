@@ -71,3 +71,12 @@ import json
 out={'R10':coeffs(chR,10),'P9':coeffs(chP,9),'P10':coeffs(chP,10),'RL6':coeffs(chL,6),'RL7':coeffs(chL,7)}
 json.dump(out,open('/tmp/cheb.json','w'))
 for k,v in out.items(): print(k,[repr(x) for x in v])
+
+# exactf.h (exact-f SC: fp32 results of fp64 evaluations, error target < 2^-46 relative):
+# e^r itself on |r| <= ln2/2, and the log series RL on [0, 0.17158^2]
+E = [F(1, math.factorial(i)) for i in range(30)]
+chE = report('E', E, -F(3466, 10000), F(3466, 10000), range(8, 12))
+out2 = {'E10': coeffs(chE, 10), 'RL5': coeffs(chL, 5)}
+json.dump(out2, open('/tmp/cheb2.json', 'w'))
+for k, v in out2.items():
+    print(k, [repr(x) for x in v])
