@@ -301,13 +301,64 @@ __device__ __forceinline__ int rank16_subb(double cv) {
     return rk;
 }
 #undef PL_RANK_ROT
+#ifndef PL_SCL_RANK_SPLIT
+#define PL_SCL_RANK_SPLIT 0  // 1: two independent borrow chains (VCC / SGPR pairs) instead of one (A/B)
+#endif
+// The same 15-rotation rank as two independent accumulations, interleaved: rotations 1..8 on the
+// VCC borrow chain of rank16_subb, rotations 9..15 as VOP3 borrow chains through SGPR pairs on
+// DPP-moved copies (5 VALU + 1 SALU each instead of 3 + 2): ~40 dependent steps instead of 75.
+#define PL_RANK_ROT_A(r, m)                                                                   \
+    "s_mov_b32 vcc_lo, " #m "\n\t"                                                          \
+    "s_mov_b32 vcc_hi, " #m "\n\t"                                                          \
+    "v_subb_co_u32_dpp %2, vcc, %7, %7, vcc row_ror:" #r " row_mask:0xf bank_mask:0xf\n\t" \
+    "v_subb_co_u32_dpp %2, vcc, %8, %8, vcc row_ror:" #r " row_mask:0xf bank_mask:0xf\n\t" \
+    "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n\t"
+#define PL_RANK_ROT_B(r, m)                                                 \
+    "v_mov_b32_dpp %3, %7 row_ror:" #r " row_mask:0xf bank_mask:0xf\n\t" \
+    "v_mov_b32_dpp %4, %8 row_ror:" #r " row_mask:0xf bank_mask:0xf\n\t" \
+    "v_subb_co_u32_e64 %3, %5, %3, %7, " #m "\n\t"                       \
+    "v_subb_co_u32_e64 %4, %6, %4, %8, %5\n\t"                           \
+    "v_addc_co_u32_e64 %1, %5, 0, %1, %6\n\t"
+__device__ __forceinline__ int rank16_split(double cv) {
+    const long long b = __double_as_longlong(cv);
+    const int lo = (int)(b & 0xffffffffLL), hi = (int)(b >> 32);
+    int ra, rb, ta, tl, th;
+    uint64_t s1, s2;
+    // static tie masks of rotations 9..15 (group lanes >= r under row_ror:r, every row)
+    constexpr uint64_t m9 = 0xfe00fe00fe00fe00ull, m10 = 0xfc00fc00fc00fc00ull, m11 = 0xf800f800f800f800ull,
+                       m12 = 0xf000f000f000f000ull, m13 = 0xe000e000e000e000ull, m14 = 0xc000c000c000c000ull,
+                       m15 = 0x8000800080008000ull;
+    asm volatile(
+        "s_nop 1\n\t"
+        "v_mov_b32 %0, 0\n\t"
+        "v_mov_b32 %1, 0\n\t"
+        PL_RANK_ROT_A(1, 0xfffefffe) PL_RANK_ROT_B(9, %9)
+        PL_RANK_ROT_A(2, 0xfffcfffc) PL_RANK_ROT_B(10, %10)
+        PL_RANK_ROT_A(3, 0xfff8fff8) PL_RANK_ROT_B(11, %11)
+        PL_RANK_ROT_A(4, 0xfff0fff0) PL_RANK_ROT_B(12, %12)
+        PL_RANK_ROT_A(5, 0xffe0ffe0) PL_RANK_ROT_B(13, %13)
+        PL_RANK_ROT_A(6, 0xffc0ffc0) PL_RANK_ROT_B(14, %14)
+        PL_RANK_ROT_A(7, 0xff80ff80) PL_RANK_ROT_B(15, %15)
+        PL_RANK_ROT_A(8, 0xff00ff00)
+        "v_add_u32 %0, %0, %1\n\t"
+        : "=&v"(ra), "=&v"(rb), "=&v"(ta), "=&v"(tl), "=&v"(th), "=&s"(s1), "=&s"(s2)
+        : "v"(lo), "v"(hi), "s"(m9), "s"(m10), "s"(m11), "s"(m12), "s"(m13), "s"(m14), "s"(m15)
+        : "vcc");
+    return ra;
+}
+#undef PL_RANK_ROT_A
+#undef PL_RANK_ROT_B
 #endif
 
 template <int GW, int r>
 __device__ __forceinline__ void rank_rot(double cv, int gl, int lane, int& rk) {
 #if PL_SCL_RANK_SUBB
     if constexpr (GW == 16 && r == 1) {
+#if PL_SCL_RANK_SPLIT
+        rk = rank16_split(cv);
+#else
         rk = rank16_subb(cv);
+#endif
         return;
     }
 #endif
@@ -540,6 +591,43 @@ __device__ void vvisit64(const St& t, int pos, bool is_g, int lane, const int* w
     constexpr int NC = 1 << V, ls = 5, h = 32, hs = 64;
     // channel rows addressed from the wave's first row (uniform base, 32-bit lane offsets)
     const float* ch0 = t.llr + t.b0 * t.n;
+#if PL_SCL_VPF
+    // software-pipelined by one element: the next element's 2 x 2^V channel values (L2) are in
+    // flight while this one's paths are evaluated (CPW * h is a multiple of 64: uniform trip count)
+    auto co_of = [&](int idx) {
+        const int c = idx >> ls, j = idx & (h - 1);
+        return (int)(t.b0 + c < t.bs ? c : t.bs - 1 - t.b0) * t.n + j;
+    };
+    float cx[NC], cy[NC];
+    {
+        const int co = co_of(lane);
+#pragma unroll
+        for (int m = 0; m < NC; ++m) {
+            cx[m] = -1.0f * ch0[co + m * hs];
+            cy[m] = -1.0f * ch0[co + h + m * hs];
+        }
+    }
+#pragma unroll 1
+    for (int idx = lane; idx < CPW * h; idx += 64) {
+        const int c = idx >> ls, j = idx & (h - 1);
+        const Cw w = t.cw(c);
+        float nx[NC], ny[NC];
+        if (idx + 64 < CPW * h) {
+            const int co = co_of(idx + 64);
+#pragma unroll
+            for (int m = 0; m < NC; ++m) {
+                nx[m] = -1.0f * ch0[co + m * hs];
+                ny[m] = -1.0f * ch0[co + h + m * hs];
+            }
+        }
+        vnode64<L, V, NS, FM>(t, w, cx, cy, wb, j, gmask, is_g, pos, ls);
+#pragma unroll
+        for (int m = 0; m < NC; ++m) {
+            cx[m] = nx[m];
+            cy[m] = ny[m];
+        }
+    }
+#else
 #pragma unroll 1
     for (int idx = lane; idx < CPW * h; idx += 64) {
         const int c = idx >> ls, j = idx & (h - 1);
@@ -553,6 +641,7 @@ __device__ void vvisit64(const St& t, int pos, bool is_g, int lane, const int* w
         }
         vnode64<L, V, NS, FM>(t, w, cx, cy, wb, j, gmask, is_g, pos, ls);
     }
+#endif
 }
 
 // One pass of a virtual node for the exact f (FM = 1, any V >= 1), where an f costs ~70 VALU and
@@ -565,6 +654,9 @@ __device__ void vvisit64(const St& t, int pos, bool is_g, int lane, const int* w
 // with a 70-instruction f).  Level q (stage s + q) combines v[m] and v[m + 2^q], m < 2^q: f when
 // the stage-(s+q) node is a left child, else g with bit base[q] + m 2^s of the path.  The same
 // operands and operations as vtree(), so the same values.
+#ifndef PL_SCL_VPF
+#define PL_SCL_VPF 0  // 1: min-sum virtual passes load the next element's channel values ahead (A/B)
+#endif
 #ifndef PL_SCL_FEX_COMBO
 #define PL_SCL_FEX_COMBO 1  // 1: the f level after the first per-path g from its four path-independent outcomes
 #endif
