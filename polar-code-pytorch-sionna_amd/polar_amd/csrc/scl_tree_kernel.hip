@@ -150,6 +150,13 @@ __host__ __device__ inline Lay make_layout(int n, int S, int L, int V) {
 // it: 16 passes at n = 1024 for the 512 values of k = 1).
 __host__ __device__ inline int chain_size(int n, int V) { return n - (n >> V); }
 __host__ __device__ inline int chain_off(int n, int k) { return n - (n >> (k - 1)); }
+// After the chain, the four-outcome tables of vvisit_ex (one per ns = 0 .. V-2): T_ns[4 e + 2 b1 + b2]
+// = f(g(src[e], src[e + 2 D], b1), g(src[e + D], src[e + 3 D], b2)), e < D = 2^(S-ns-2), src = the
+// channel (ns = 0) or chain level ns.  Every pass with the same ns reads the same table (8 passes
+// for ns = 0 at n = 1024), so it is evaluated once per codeword.
+__host__ __device__ inline int combo_size(int n, int V) { return V >= 2 ? 2 * n - 4 * (n >> V) : 0; }
+__host__ __device__ inline int combo_off(int n, int V, int ns) { return chain_size(n, V) + 2 * n - 4 * (n >> (ns + 1)); }
+__host__ __device__ inline int cache_size(int n, int V) { return chain_size(n, V) + combo_size(n, V); }
 
 #if PL_SCL_FG_BITS
 // v_min_f64 without the input canonicalisation fmin() adds (a v_max_f64 per operand that is not
@@ -712,16 +719,40 @@ __device__ PL_FEX_PASS_ATTR void vvisit_ex(const float* __restrict__ llr, int64_
         // shared level-ns values (ns > 0), or the four-outcome table w[m + (2 b1 + b2) h2] (combo).
         wv wx, wy;
         int hh = NC;
-        if (ns == 0 || vcache == nullptr) {
+        const bool tab = combo && vcache != nullptr;  // the four-outcome table from the workspace
+        if (tab) {
+            const double* tb = vcache + c * cache_size(n, V) + combo_off(n, V, ns);
+            auto load = [&](auto H2c) {
+                constexpr int H2 = decltype(H2c)::value;
+#pragma unroll
+                for (int m = 0; m < H2; ++m) {
+                    const double* ox = tb + 4 * (j + m * hs);
+                    const double* oy = tb + 4 * (j + h + m * hs);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        wx[m + k * H2] = ox[k];
+                        wy[m + k * H2] = oy[k];
+                    }
+                }
+            };
+            if constexpr (H >= 8) {
+                if (h2 == 4) load(std::integral_constant<int, (H >= 8 ? 4 : 1)>{});
+            }
+            if constexpr (H >= 4) {
+                if (h2 == 2) load(std::integral_constant<int, (H >= 4 ? 2 : 1)>{});
+            }
+            if (h2 == 1) load(std::integral_constant<int, 1>{});
+        } else if (ns == 0 || vcache == nullptr) {
 #pragma unroll
             for (int m = 0; m < NC; ++m) {
                 wx[m] = (double)(-1.0f * ch0[co + m * hs]);  // negated (polar_scl.py:219)
                 wy[m] = (double)(-1.0f * ch0[co + h + m * hs]);
             }
         }
-        if (ns > 0 && vcache != nullptr) {  // level ns of the leftmost chain: element j + m 2^s (x), + h (y)
+        if (tab) {
+        } else if (ns > 0 && vcache != nullptr) {  // level ns of the leftmost chain: element j + m 2^s (x), + h (y)
             hh = NC >> ns;
-            const double* cb = vcache + c * chain_size(n, V) + chain_off(n, ns) + j;
+            const double* cb = vcache + c * cache_size(n, V) + chain_off(n, ns) + j;
 #pragma unroll
             for (int m = 0; m < H; ++m) {
                 if (m < hh) {
@@ -742,7 +773,7 @@ __device__ PL_FEX_PASS_ATTR void vvisit_ex(const float* __restrict__ llr, int64_
                 }
             }
         }
-        if (combo) {  // in place: block m reads and writes exactly the indices m + k h2, k < 4
+        if (combo && !tab) {  // in place: block m reads and writes exactly the indices m + k h2, k < 4
 #pragma unroll 1
             for (int m = 0; m < h2; ++m) {
                 const double xa = wx[m], xb = wx[m + h1], xc_ = wx[m + h2], xd = wx[m + h2 + h1];
@@ -890,6 +921,26 @@ __device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane) {
     } else if (PL_SCL_ST_UNROLL && FM == 0 && s <= t.SS && ls <= R + 1) {  // exact f: spills (7.7 -> 11.2 ms)
         if (ls == R) node_fg_st<L, FM, CPW, R>(t, pos, is_g, lane);
         else node_fg_st<L, FM, CPW, R + 1>(t, pos, is_g, lane);
+    } else if (FM == 1 && s <= t.SS && !is_g && (CPW * L * h) % 128 == 0) {
+        // exact f, stored stage: two elements per lane per step, their f chains interleaved
+        const int total = CPW * L * h;
+        for (int i0 = lane; i0 < total; i0 += 128) {
+            double x[2], y[2], r[2];
+            double* o[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int idx = i0 + 64 * u;
+                const int c = idx >> (LL + ls), p = (idx >> ls) & (L - 1), j = idx & (h - 1);
+                const Cw w = t.cw(c);
+                const double* in = w.A + w.sptr[p * SPS + s] * t.per + (1 << s) - (1 << R);
+                x[u] = in[j];
+                y[u] = in[j + h];
+                o[u] = w.A + p * t.per + (1 << ls) - (1 << R) + j;
+            }
+            f_ex2(x[0], y[0], x[1], y[1], t.lmax, r[0], r[1]);
+            *o[0] = r[0];
+            *o[1] = r[1];
+        }
     } else if (s <= t.SS) {
         const int total = CPW * L * h;
         for (int idx = lane; idx < total; idx += 64) {
@@ -1578,7 +1629,7 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
     t.SS = t.y.SS;
     t.per = t.y.per;
     t.lmax = lmax;
-    t.vcache = (FM == 1 && V >= 1 && vcache != nullptr) ? vcache + t.b0 * chain_size(n, V) : nullptr;
+    t.vcache = (FM == 1 && V >= 1 && vcache != nullptr) ? vcache + t.b0 * cache_size(n, V) : nullptr;
     const int W = t.W, LW = ilog2(W);
     const int gl = lane & (GW - 1), my_c = lane / GW;
     const Cw mine = t.cw(my_c);
@@ -1597,7 +1648,7 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
 
     if constexpr (FM == 1 && V >= 1) {
         if (t.vcache != nullptr) {  // fill the leftmost chain, level by level (wave-parallel, pairs of f)
-            const int cs = chain_size(n, V);
+            const int cs = cache_size(n, V);
 #pragma unroll 1
             for (int k = 1; k <= V; ++k) {
                 const int sz = n >> k, lsz = S - k;
@@ -1629,6 +1680,44 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
                 __threadfence_block();
                 __syncthreads();
             }
+#if PL_SCL_FEX_COMBO
+#pragma unroll 1
+            for (int ns = 0; ns + 2 <= V; ++ns) {  // the four-outcome tables (combo_off)
+                const int D = n >> (ns + 2), lsz = S - ns - 2;
+                const double* src = t.vcache + chain_off(n, ns > 0 ? ns : 1);
+                double* tab = t.vcache + combo_off(n, V, ns);
+#pragma unroll 1
+                for (int idx = lane; idx < CPW * D; idx += 64) {
+                    const int c = idx >> lsz, e = idx & (D - 1);
+                    double a, b, cc, d;
+                    if (ns == 0) {
+                        const float* ch = t.cw(c).ch;
+                        a = (double)(-1.0f * ch[e]);
+                        b = (double)(-1.0f * ch[e + 2 * D]);
+                        cc = (double)(-1.0f * ch[e + D]);
+                        d = (double)(-1.0f * ch[e + 3 * D]);
+                    } else {
+                        const double* sc = src + c * cs;
+                        a = sc[e];
+                        b = sc[e + 2 * D];
+                        cc = sc[e + D];
+                        d = sc[e + 3 * D];
+                    }
+                    const double g0 = g_op(a, b, 0u), g1 = g_op(a, b, 1u);
+                    const double h0 = g_op(cc, d, 0u), h1 = g_op(cc, d, 1u);
+                    double r0, r1, r2, r3;
+                    f_ex2(g0, h0, g0, h1, t.lmax, r0, r1);
+                    f_ex2(g1, h0, g1, h1, t.lmax, r2, r3);
+                    double* o = tab + c * cs + 4 * e;
+                    o[0] = r0;
+                    o[1] = r1;
+                    o[2] = r2;
+                    o[3] = r3;
+                }
+            }
+            __threadfence_block();
+            __syncthreads();
+#endif
         }
     }
 
@@ -1836,7 +1925,7 @@ size_t scl_tree_workspace_size(const pl_plan* p, int64_t bs) {
     if (V < 1) return 0;
     const int cpw = 32 / p->list_size;
     const int64_t slots = (bs + cpw - 1) / cpw * cpw;
-    return (size_t)slots * (size_t)chain_size(p->n, V) * sizeof(double);
+    return (size_t)slots * (size_t)cache_size(p->n, V) * sizeof(double);
 }
 
 int launch_scl_tree(const pl_plan* p, const float* llr, int64_t bs, void* out, int out_kind, double* out_pm,

@@ -231,9 +231,9 @@ def test_scl_n2048_module_and_limits(pa):
 
 @pytest.mark.parametrize("n,k,fast", [(1024, 512, True), (1024, 512, False), (512, 256, True), (256, 128, True)])
 def test_exact_scl_chain_cache_is_transparent(pa, n, k, fast):
-    """The exact-f subtree kernel's leftmost-chain cache (the pl_scl_decode workspace) changes no
-    bit and no metric: decoding with the workspace equals decoding with NULL (the chain recomputed
-    in every virtual pass), including a tail wave (bs not a multiple of the codewords per wave)."""
+    """The exact-f subtree kernel's workspace caches (leftmost chain, four-outcome tables) change no
+    bit and no metric: decoding with the workspace equals decoding with NULL (both recomputed in
+    every virtual pass), including a tail wave (bs not a multiple of the codewords per wave)."""
     import ctypes
 
     from polar_amd import _lib, ops
@@ -241,7 +241,9 @@ def test_exact_scl_chain_cache_is_transparent(pa, n, k, fast):
     flags = _lib.PL_PLAN_FAST_SCL if fast else 0
     plan = _lib.Plan(n, pa.frozen_mask(fp, n), 8, _lib.PL_F_EXACT, flags=flags)
     bs = 67
-    assert int(_lib.lib().pl_scl_workspace_size(plan.handle, bs)) == 68 * (n - (n >> plan_v(n))) * 8
+    v = plan_v(n)  # per codeword: the leftmost chain, then the four-outcome tables (scl_tree_kernel.hip)
+    per_cw = (n - (n >> v)) + (2 * n - 4 * (n >> v) if v >= 2 else 0)
+    assert int(_lib.lib().pl_scl_workspace_size(plan.handle, bs)) == 68 * per_cw * 8
     g = torch.Generator(device="cuda").manual_seed(n + fast)
     llr = (torch.randn((bs, n), device="cuda", generator=g) * 2.0 + 0.8).contiguous()
     bits, pm = ops.scl_decode(plan, llr, return_pm=True)
