@@ -88,4 +88,24 @@ __device__ __attribute__((noinline)) float f_exact(float x, float y, float lmax)
     return o;
 }
 
+// Two f at once (one call, the two evaluations' fp64 chains interleaved by the scheduler): the
+// specialised SC kernel's lane-local f loops call this for element pairs.  Each value is exactly
+// f_exact's.
+struct f2 {
+    float a, b;
+};
+__device__ __attribute__((noinline)) f2 f_exact2(float x0, float y0, float x1, float y1, float lmax) {
+    const float xc0 = fminf(fmaxf(x0, -lmax), lmax), yc0 = fminf(fmaxf(y0, -lmax), lmax);
+    const float xc1 = fminf(fmaxf(x1, -lmax), lmax), yc1 = fminf(fmaxf(y1, -lmax), lmax);
+    const float s0 = exp_cr(xc0 + yc0), s1 = exp_cr(xc1 + yc1);
+    const float a0 = exp_cr(xc0), a1 = exp_cr(xc1);
+    const float b0 = exp_cr(yc0), b1 = exp_cr(yc1);
+    const float p0 = log_cr(1.0f + s0), p1 = log_cr(1.0f + s1);
+    const float q0 = log_cr(a0 + b0), q1 = log_cr(a1 + b1);
+    f2 r;
+    r.a = p0 - q0;
+    r.b = p1 - q1;
+    return r;
+}
+
 }  // namespace plx

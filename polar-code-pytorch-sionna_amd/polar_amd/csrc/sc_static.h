@@ -235,6 +235,25 @@ __device__ __forceinline__ float fop(float x, float y, float lmax) {
         return plx::f_exact(x, y, lmax);  // my_sn dec.py:39-43, correctly rounded exp / log (exactf.h)
     }
 }
+// x[j] = f(a[j], a[j + H]), j < H.  Exact f: element pairs through plx::f_exact2 (half the
+// calls, two interleaved evaluations per call).
+#ifndef PL_SC_FEX_PAIR
+#define PL_SC_FEX_PAIR 1
+#endif
+template <int FM, bool BND, int H>
+__device__ __forceinline__ void fvec(const float* a, float* x, float lmax) {
+    if constexpr (FM == 1 && H >= 2 && PL_SC_FEX_PAIR) {
+#pragma unroll
+        for (int j = 0; j < H; j += 2) {
+            const plx::f2 r = plx::f_exact2(a[j], a[j + H], a[j + 1], a[j + 1 + H], lmax);
+            x[j] = r.a;
+            x[j + 1] = r.b;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < H; ++j) x[j] = fop<FM, BND>(a[j], a[j + H], lmax);
+    }
+}
 // g, polar_sc.py:49-53: (1-2u)x + y == (u ? -x : x) + y, one rounding.  The flip is the sign
 // bit (bit 31) of t; bitop3 S1 ^ (S0 & S2) (table 0x6c) applies it in one op.
 __device__ __forceinline__ float flip31(float x, uint32_t t) {
@@ -516,8 +535,7 @@ __device__ __forceinline__ BV<(1 << s) / C::G> split(const float (&a)[(1 << s) /
     float x[H];
     BV<H> bl = bzero<H>();
     if constexpr (nt<C>(s - 1, P) != R0) {
-#pragma unroll
-        for (int j = 0; j < H; ++j) x[j] = fop<C::FM, lchild<C>(s, P)>(a[j], a[j + H], ln.lmax);
+        fvec<C::FM, lchild<C>(s, P), H>(a, x, ln.lmax);
         bl = child<C, s, P>(x, ln);
         gvec<H>(a, bl, x);
     } else {
@@ -704,8 +722,7 @@ __device__ __forceinline__ Beta<C::NS / 2> half(float (&ch)[C::NS], uint64_t blr
         float va[E];
         valphas<C, SIDE>(ch, blr, va, ln.lmax);
         if constexpr (nt<C>(s - 1, P) != R0) {
-#pragma unroll
-            for (int j = 0; j < H; ++j) x[j] = fop<C::FM, SIDE == 0>(va[j], va[j + H], ln.lmax);
+            fvec<C::FM, SIDE == 0, H>(va, x, ln.lmax);
             bl = child<C, s, P>(x, ln);
 #if PL_SC_VA_RECOMPUTE
             // recompute the virtual LLRs for the g pass instead of keeping them live across the
