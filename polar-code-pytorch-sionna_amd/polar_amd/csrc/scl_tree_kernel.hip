@@ -309,7 +309,7 @@ __device__ __forceinline__ int rank16_subb(double cv) {
 }
 #undef PL_RANK_ROT
 #ifndef PL_SCL_RANK_SPLIT
-#define PL_SCL_RANK_SPLIT 0  // 1: two independent borrow chains (VCC / SGPR pairs) instead of one (A/B)
+#define PL_SCL_RANK_SPLIT 1  // 1: two independent borrow chains (VCC / SGPR pairs) instead of one (A/B r03u: 0.985 vs 0.991 ms)
 #endif
 // The same 15-rotation rank as two independent accumulations, interleaved: rotations 1..8 on the
 // VCC borrow chain of rank16_subb, rotations 9..15 as VOP3 borrow chains through SGPR pairs on
@@ -361,11 +361,7 @@ template <int GW, int r>
 __device__ __forceinline__ void rank_rot(double cv, int gl, int lane, int& rk) {
 #if PL_SCL_RANK_SUBB
     if constexpr (GW == 16 && r == 1) {
-#if PL_SCL_RANK_SPLIT
-        rk = rank16_split(cv);
-#else
         rk = rank16_subb(cv);
-#endif
         return;
     }
 #endif
@@ -1209,7 +1205,7 @@ __device__ __forceinline__ void pull_live(double* st, int i, int src) {
 // candidate to the group lane of its rank (ranks are a permutation of [0, 2L), so every lane is
 // written exactly once), and slots >= L re-shadow slot - L.  Returns the lane's new metric, the
 // path (group index) it descends from and the bit the candidate appended.
-template <int L>
+template <int L, int FM>
 __device__ __forceinline__ void select_2l(double cv, int gl, int gbase, int lane, double& npm, int& par,
                                           uint32_t& bit) {
     constexpr int GW = 2 * L;
@@ -1226,6 +1222,8 @@ __device__ __forceinline__ void select_2l(double cv, int gl, int gbase, int lane
             const double v = readlane_d(cv, c);
             rk += (v < cv || (v == cv && c < lane)) ? 1 : 0;
         }
+    } else if constexpr (GW == 16 && FM == 0 && PL_SCL_RANK_SUBB && PL_SCL_RANK_SPLIT) {
+        rk = rank16_split(cv);  // min-sum kernels only: its 14 mask SGPRs spill the exact-f ones
     } else {
         rank_rot<GW, 1>(cv, gl, lane, rk);
     }
@@ -1373,7 +1371,7 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
                     double npm;
                     int par;
                     uint32_t bit;
-                    select_2l<L>(pm + nsum, gl, gbase, lane, npm, par, bit);
+                    select_2l<L, FM>(pm + nsum, gl, gbase, lane, npm, par, bit);
                     pm = npm;
                     ps = (uint32_t)bperm_i((int)ps, gbase + par) | (bit << last);
                     org = bperm_i(org, gbase + par);
@@ -1414,7 +1412,7 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
         double npm;
         int par;
         uint32_t bit;
-        select_2l<L>(pm + pen, gl, gbase, lane, npm, par, bit);
+        select_2l<L, FM>(pm + pen, gl, gbase, lane, npm, par, bit);
         pm = npm;
         ps = (uint32_t)bperm_i((int)ps, gbase + par) | (bit << i);
         org = bperm_i(org, gbase + par);
@@ -1591,7 +1589,7 @@ __device__ void upper_prune(const St& t, int s, int pos, int kind, double& pm, i
     double npm;
     int par;
     uint32_t bit;
-    select_2l<L>(pm + nsum, gl, gbase, lane, npm, par, bit);
+    select_2l<L, FM>(pm + nsum, gl, gbase, lane, npm, par, bit);
     pm = npm;
     if (gl < L) w.org_s[gl] = par;
     __syncthreads();

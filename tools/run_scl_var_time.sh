@@ -4,5 +4,5 @@ cd $GRAFT_REPO_ROOT
 for cfg in "$@"; do
   set -- $cfg
   echo "SCL_FMODE=$1 SCL_FLAGS=$2"
-  SCL_FMODE=$1 SCL_FLAGS=$2 SCL_ROUNDS=2 timeout -k 10 300 python -u tools/scl_variants.py time || exit $?
+  SCL_FMODE=$1 SCL_FLAGS=$2 SCL_ROUNDS=${SCL_ROUNDS:-2} timeout -k 10 300 python -u tools/scl_variants.py time || exit $?
 done
