@@ -4,12 +4,14 @@
 // Shared by scl_kernel.hip and scl_tree_kernel.hip so the two kernels produce identical metrics.
 // Same three roundings as the reference -- e = exp(z), y = 1 + e, log(y) -- with exp and log
 // evaluated for the range the decoder uses instead of through ocml's general routines:
-//   exp: z = k ln2 + r (Cody-Waite, two-part ln2 with FMA), |r| <= ln2/2, Taylor polynomial of
-//        degree 13 (truncation < 5e-18 relative), scaled by 2^k;
-//   log: y = 2^e m, m in [sqrt(1/2), sqrt(2)), log m = 2 atanh(s), s = (m-1)/(m+1), |s| < 0.1716,
-//        series through s^25 (truncation < 1e-18 relative).
-// Both are within ~2 ulp of the correctly rounded result, like ocml's and numpy's.  Valid for
-// |z| <= 700: pl_plan_create rejects list plans with llr_max > 700.
+//   exp: z = k ln2 + r (Cody-Waite, two-part ln2 with FMA), |r| <= ln2/2, a polynomial, scaled
+//        by 2^k;
+//   log: y = 2^e m, m in [sqrt(1/2), sqrt(2)), log m = 2 atanh(s), s = (m-1)/(m+1), |s| < 0.1716.
+// The default (PL_SP_FORM 2, below softplus_pm) uses Chebyshev-economised polynomials evaluated
+// in Estrin form and a Newton reciprocal for s; the Taylor forms of rounds 1-2 (pm_exp / pm_log,
+// degree 13 and s^25) remain as PL_SP_FORM 0.  Both are within ~1.5 ulp of the correctly rounded
+// exp and log, like ocml's and numpy's.  Valid for |z| <= 700: pl_plan_create rejects list plans
+// with llr_max > 700.  The exact boxplus of the my_sn list decoder (f_exact_pm_n) is at the end.
 #pragma once
 #include <hip/hip_runtime.h>
 
