@@ -102,9 +102,9 @@ int pl_sc_decode(const pl_plan* plan, const float* llr_logits, int64_t bs, void*
 
 /* SCL decode.  out_pm (nullable): [bs, 2L] fp64, the reference's final sorted msg_pm.
  * workspace: device scratch of pl_scl_workspace_size(plan, bs) bytes -- the exact-f list kernels
- * keep a path-independent cache of the upper tree there (bs * 7.5 KB at n = 1024).  NULL with
- * ws_bytes 0 runs without it (same results, slower); a non-NULL workspace smaller than the size
- * is PL_EINVAL. */
+ * keep path-independent caches of the upper tree there (22 KB per codeword at n = 1024, for at
+ * most 16384 codewords: larger batches are decoded in chunks over it).  NULL with ws_bytes 0 runs
+ * without them (same results, slower); a non-NULL workspace smaller than the size is PL_EINVAL. */
 size_t pl_scl_workspace_size(const pl_plan* plan, int64_t bs);
 int pl_scl_decode(const pl_plan* plan, const float* llr_logits, int64_t bs, void* out_bits,
                   int32_t out_kind, double* out_pm, void* workspace, size_t ws_bytes,

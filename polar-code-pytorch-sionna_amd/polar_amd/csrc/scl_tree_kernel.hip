@@ -1915,14 +1915,19 @@ bool scl_tree_eligible(const pl_plan* p) {
     return p->list_size >= 2 && p->list_size <= 32 && p->log_n >= 5 && p->log_n <= 10;
 }
 
-// Workspace: the exact-f kernels' leftmost-chain cache, one slot per codeword of every launched
-// wave (a tail wave's clamped codewords get their own slots).
+// Workspace: the exact-f kernels' leftmost-chain cache and four-outcome tables, one slot per
+// codeword of every launched wave (a tail wave's clamped codewords get their own slots).  A batch
+// larger than kSclWsChunk codewords is decoded as consecutive launches of kSclWsChunk (each two
+// full rounds of the chip's 2048 resident waves at L = 8) that reuse one chunk's workspace:
+// 22 KB per codeword at n = 1024 bounds it to 360 MB whatever the batch.
+constexpr int64_t kSclWsChunk = 16384;
 size_t scl_tree_workspace_size(const pl_plan* p, int64_t bs) {
     if (!scl_tree_eligible(p) || p->f_mode != PL_F_EXACT || bs <= 0) return 0;
     const int V = pick_v(p->log_n);
     if (V < 1) return 0;
     const int cpw = 32 / p->list_size;
-    const int64_t slots = (bs + cpw - 1) / cpw * cpw;
+    const int64_t b = bs < kSclWsChunk ? bs : kSclWsChunk;  // larger batches run in chunks of kSclWsChunk
+    const int64_t slots = (b + cpw - 1) / cpw * cpw;
     return (size_t)slots * (size_t)cache_size(p->n, V) * sizeof(double);
 }
 
@@ -1966,11 +1971,19 @@ int launch_scl_tree(const pl_plan* p, const float* llr, int64_t bs, void* out, i
     const int32_t* ip = p->d_info_pos;
     double* vc = ws_bytes >= scl_tree_workspace_size(p, bs) && scl_tree_workspace_size(p, bs) > 0
                      ? static_cast<double*>(ws) : nullptr;
-    void* args[] = {(void*)&llr, (void*)&bs, (void*)&out, (void*)&out_kind, (void*)&out_pm, (void*)&fw,
-                    (void*)&ip, (void*)&n, (void*)&S, (void*)&k, (void*)&lmax, (void*)&cdeg, (void*)&cg, (void*)&vc};
-    const int64_t blocks = (bs + cpw - 1) / cpw;
-    hipError_t e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(64), args, lds, st);
-    if (e != hipSuccess) return check_hip(e, "SCL decode launch (subtree kernel)");
+    const int64_t chunk = vc != nullptr ? kSclWsChunk : bs;  // the workspace holds one chunk's slots
+    const size_t out_elem = out_kind == PL_OUT_F32 ? sizeof(float) : sizeof(uint8_t);
+    for (int64_t off = 0; off < bs; off += chunk) {
+        int64_t cbs = bs - off < chunk ? bs - off : chunk;
+        const float* cllr = llr + off * n;
+        void* cout = static_cast<unsigned char*>(out) + (size_t)off * (size_t)k * out_elem;
+        double* cpm = out_pm != nullptr ? out_pm + off * 2 * L : nullptr;
+        void* args[] = {(void*)&cllr, (void*)&cbs, (void*)&cout, (void*)&out_kind, (void*)&cpm, (void*)&fw,
+                        (void*)&ip, (void*)&n, (void*)&S, (void*)&k, (void*)&lmax, (void*)&cdeg, (void*)&cg, (void*)&vc};
+        const int64_t blocks = (cbs + cpw - 1) / cpw;
+        hipError_t e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(64), args, lds, st);
+        if (e != hipSuccess) return check_hip(e, "SCL decode launch (subtree kernel)");
+    }
     return check_hip(hipGetLastError(), "SCL decode launch (subtree kernel)");
 }
 

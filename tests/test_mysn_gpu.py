@@ -265,3 +265,29 @@ def plan_v(n):
     if v == 4 and S != 10:
         v = 3
     return max(v, 0)
+
+
+def test_exact_scl_workspace_chunks(pa):
+    """A batch above the workspace chunk (16384 codewords) runs as consecutive launches over one
+    chunk-sized workspace: the same bits and metrics as one launch without the workspace, and the
+    workspace size stops growing with the batch."""
+    import ctypes
+
+    from polar_amd import _lib, ops
+    n, k = 256, 128
+    fp = pa.reference_frozen_pos(k, n).numpy()
+    plan = _lib.Plan(n, pa.frozen_mask(fp, n), 8, _lib.PL_F_EXACT, flags=_lib.PL_PLAN_FAST_SCL)
+    L = _lib.lib()
+    assert int(L.pl_scl_workspace_size(plan.handle, 16384)) == int(L.pl_scl_workspace_size(plan.handle, 40000))
+    bs = 16384 + 37
+    g = torch.Generator(device="cuda").manual_seed(11)
+    llr = (torch.randn((bs, n), device="cuda", generator=g) * 2.0 + 0.8).contiguous()
+    bits, pm = ops.scl_decode(plan, llr, return_pm=True)
+    out = torch.empty((bs, k), device="cuda")
+    pm0 = torch.empty((bs, 16), device="cuda", dtype=torch.float64)
+    _lib.check(L.pl_scl_decode(plan.handle, ctypes.c_void_p(llr.data_ptr()), bs, ctypes.c_void_p(out.data_ptr()),
+                               _lib.PL_OUT_F32, ctypes.c_void_p(pm0.data_ptr()), None, 0,
+                               _lib.current_stream_ptr(llr.device)), "pl_scl_decode")
+    torch.cuda.synchronize()
+    assert torch.equal(bits, out)
+    assert torch.equal(pm, pm0)
