@@ -31,6 +31,7 @@ def lib():
         P = ctypes.c_void_p
         i32, i64 = ctypes.c_int, ctypes.c_int64
         L.orc_sc_decode.argtypes = [i32, P, i32, P, i64, P, i32]
+        L.orc_sc_decode_lmax.argtypes = [i32, P, i32, ctypes.c_float, P, i64, P, i32]
         L.orc_scl_decode.argtypes = [i32, P, i32, P, i64, P, P, i32]
         L.orc_scl_decode_lazy.argtypes = [i32, P, i32, P, i64, P, P, i32]
         L.orc_polar_encode.argtypes = [i32, P, P, i64, P]
@@ -40,7 +41,7 @@ def lib():
         L.orc_crc_check.argtypes = [P, i64, i32, i32, ctypes.c_uint32, P]
         L.orc_np_pairwise_sum.argtypes = [P, i32]
         L.orc_np_pairwise_sum.restype = ctypes.c_double
-        for f in (L.orc_sc_decode, L.orc_scl_decode, L.orc_scl_decode_lazy, L.orc_polar_encode,
+        for f in (L.orc_sc_decode, L.orc_sc_decode_lmax, L.orc_scl_decode, L.orc_scl_decode_lazy, L.orc_polar_encode,
                   L.orc_scl_decode_mysn, L.orc_crc_encode, L.orc_crc_check):
             f.restype = i32
         _lib = L
@@ -57,15 +58,16 @@ def _ptr(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 
 
-def sc_decode(llr_logits, frozen_pos, f_mode=0, nthreads=0):
+def sc_decode(llr_logits, frozen_pos, f_mode=0, nthreads=0, llr_max=30.0):
     """SC decode (polar_sc.py SC_Dec semantics).  llr_logits: [bs, n] float32 logits.
-    Returns float32 [bs, k] 0/1 bits."""
+    Returns float32 [bs, k] 0/1 bits.  llr_max: the clipping bound (the reference's is 30)."""
     x = np.ascontiguousarray(llr_logits, dtype=np.float32)
     bs, n = x.shape
     fm = frozen_mask(frozen_pos, n)
     k = int(n - fm.sum())
     out = np.empty((bs, k), dtype=np.float32)
-    r = lib().orc_sc_decode(n, _ptr(fm), int(f_mode), _ptr(x), bs, _ptr(out), int(nthreads))
+    r = lib().orc_sc_decode_lmax(n, _ptr(fm), int(f_mode), ctypes.c_float(llr_max), _ptr(x), bs, _ptr(out),
+                                 int(nthreads))
     if r < 0:
         raise ValueError("orc_sc_decode rejected its arguments")
     return out

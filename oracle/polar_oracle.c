@@ -40,16 +40,17 @@
 #define LLR_MAX 30.0f
 
 static inline float clipf(float x) { return fminf(fmaxf(x, -LLR_MAX), LLR_MAX); }
+static inline float clipf_l(float x, float l) { return fminf(fmaxf(x, -l), l); }
 static inline float signf_t(float x) { return (float)((x > 0.0f) - (x < 0.0f)); } /* torch.sign */
 
 /* f, polar_sc.py:33-48: min-sum is what runs (line 46 overrides the exact result). */
-static inline float f_minsum(float x, float y) {
-    float xc = clipf(x), yc = clipf(y);
+static inline float f_minsum(float x, float y, float l) {
+    float xc = clipf_l(x, l), yc = clipf_l(y, l);
     return signf_t(xc) * signf_t(yc) * fminf(fabsf(xc), fabsf(yc));
 }
 /* f, my_sn/fec/polar/dec.py:33-46: exact log-domain boxplus on clipped inputs (fp32). */
-static inline float f_exact(float x, float y) {
-    float xc = clipf(x), yc = clipf(y);
+static inline float f_exact(float x, float y, float l) {
+    float xc = clipf_l(x, l), yc = clipf_l(y, l);
     float o = logf(1.0f + expf(xc + yc));
     o -= logf(expf(xc) + expf(yc));
     return o;
@@ -64,6 +65,7 @@ static int ilog2(int n) { int s = 0; while ((1 << s) < n) ++s; return ((1 << s) 
 /* ---------------------------------------------------------------- SC ---- */
 typedef struct {
     int n, S, f_mode;
+    float lmax;   /* llr_max (the reference: 30) */
     const uint8_t* frozen;
     float* llr;   /* [S+1][n]  msg_llr  (polar_sc.py:108-110) */
     float* uhat;  /* [S+1][n]  msg_uhat */
@@ -79,7 +81,8 @@ static void sc_node(sc_ctx* c, int a, int s) {
         float* in = L + (size_t)s * n;
         float* out = L + (size_t)(s - 1) * n;
         for (int j = 0; j < h; ++j)
-            out[a + j] = c->f_mode ? f_exact(in[a + j], in[a + h + j]) : f_minsum(in[a + j], in[a + h + j]);
+            out[a + j] = c->f_mode ? f_exact(in[a + j], in[a + h + j], c->lmax)
+                                : f_minsum(in[a + j], in[a + h + j], c->lmax);
         sc_node(c, a, s - 1);
         const float* ul = U + (size_t)(s - 1) * n;
         for (int j = 0; j < h; ++j) out[a + h + j] = g_op(in[a + j], in[a + h + j], ul[a + j]);
@@ -95,9 +98,11 @@ static void sc_node(sc_ctx* c, int a, int s) {
     }
 }
 
-/* SC_Dec.forward (polar_sc.py:113-133): logits are negated, decoded, gathered at info_pos. */
-int orc_sc_decode(int n, const uint8_t* frozen_mask, int f_mode, const float* logits, int64_t bs,
-                  float* out_bits, int nthreads) {
+/* SC_Dec.forward (polar_sc.py:113-133): logits are negated, decoded, gathered at info_pos.
+ * orc_sc_decode_lmax: the same with another clipping bound than the reference's 30 (a plan's
+ * llr_max; tests of the full-range exact f). */
+int orc_sc_decode_lmax(int n, const uint8_t* frozen_mask, int f_mode, float lmax, const float* logits, int64_t bs,
+                       float* out_bits, int nthreads) {
     const int S = ilog2(n);
     if (S < 0 || !frozen_mask || !logits || !out_bits || bs < 0) return -1;
     int* info = (int*)malloc(sizeof(int) * (size_t)n);
@@ -109,7 +114,7 @@ int orc_sc_decode(int n, const uint8_t* frozen_mask, int f_mode, const float* lo
 #endif
     {
         sc_ctx c;
-        c.n = n; c.S = S; c.f_mode = f_mode; c.frozen = frozen_mask;
+        c.n = n; c.S = S; c.f_mode = f_mode; c.lmax = lmax; c.frozen = frozen_mask;
         c.llr = (float*)malloc(sizeof(float) * (size_t)(S + 1) * n);
         c.uhat = (float*)malloc(sizeof(float) * (size_t)(S + 1) * n);
 #ifdef _OPENMP
@@ -125,6 +130,10 @@ int orc_sc_decode(int n, const uint8_t* frozen_mask, int f_mode, const float* lo
     }
     free(info);
     return k;
+}
+int orc_sc_decode(int n, const uint8_t* frozen_mask, int f_mode, const float* logits, int64_t bs,
+                  float* out_bits, int nthreads) {
+    return orc_sc_decode_lmax(n, frozen_mask, f_mode, LLR_MAX, logits, bs, out_bits, nthreads);
 }
 
 /* --------------------------------------------------------------- SCL ---- */

@@ -42,6 +42,29 @@ def _needs(obj, src, deps):
     return any(os.path.getmtime(d) > t for d in [src] + deps)
 
 
+def source_hash():
+    """FNV-1a 64 over the library's sources (csrc/*, the C header) in name order: pl_version()
+    reports it, so a prebuilt library that travels without its sources can be matched to them."""
+    h = 0xcbf29ce484222325
+    files = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp", ".h")))
+    paths = [os.path.join(CSRC, f) for f in files] + [os.path.join(HERE, "..", "..", "include", "polar_mi355x.h")]
+    for path in paths:
+        for b in os.path.basename(path).encode() + b"\0" + open(path, "rb").read():
+            h = ((h ^ b) * 0x100000001b3) & 0xFFFFFFFFFFFFFFFF
+    return f"{h:016x}"
+
+
+def _write_src_hash(obj_dir):
+    """obj_dir/src_hash.h: the source hash as PL_SRC_HASH (rewritten only when it changes, so
+    capi.cpp rebuilds exactly when a source does)."""
+    path = os.path.join(obj_dir, "src_hash.h")
+    text = f'#define PL_SRC_HASH "{source_hash()}"\n'
+    if not os.path.exists(path) or open(path).read() != text:
+        with open(path, "w") as f:
+            f.write(text)
+    return path
+
+
 def _embed_static_source():
     """sc_static.h as a C++ raw string literal (the hiprtc source of the specialised kernels)."""
     src = open(os.path.join(CSRC, "sc_static.h")).read()
@@ -71,17 +94,18 @@ def build(force=False, verbose=False, dev=False):
     dev_flags = ["-DPL_DEV=1"] if dev else []
     os.makedirs(obj_dir, exist_ok=True)
     inc = _embed_static_source()
+    hash_h = _write_src_hash(obj_dir)
     deps = [os.path.join(CSRC, "plan.h"), os.path.join(CSRC, "softplus.h"), os.path.join(CSRC, "exactf.h"),
             os.path.join(HERE, "..", "..", "include", "polar_mi355x.h")]
     jobs = []
     for oname, s, defs in UNITS:
         src = os.path.join(CSRC, s)
         obj = os.path.join(obj_dir, oname)
-        extra = [inc] if s == "jit.cpp" else []
+        extra = [inc] if s == "jit.cpp" else [hash_h] if s == "capi.cpp" else []
         if force or _needs(obj, src, deps + extra):
             lang = ["-x", "hip"] if s.endswith(".cpp") else []
             cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-                   "-ffp-contract=off", f"-I{OBJ}", *dev_flags, *defs, *lang, "-c", src, "-o", obj]
+                   "-ffp-contract=off", f"-I{obj_dir}", f"-I{OBJ}", *dev_flags, *defs, *lang, "-c", src, "-o", obj]
             jobs.append(cmd)
 
     def run(cmd):
@@ -220,6 +244,10 @@ def reference_codes():
     out += [(m, 0) for _, m in root_half_codes()]
     # tests/test_sc_gpu.py::test_sc_edge_cases: n = 64 with every position frozen (k = 0) and none (k = n)
     out += [(np.ones(64, dtype=np.uint8), 0), (np.zeros(64, dtype=np.uint8), 0)]
+    # tests/test_sc_gpu.py::test_sc_exact_large_llr_max_*: every n = 2, 4 code with k >= 1, exact f
+    for n in (2, 4):
+        for code in range(1, 1 << n):
+            out.append((np.array([((code >> i) & 1) ^ 1 for i in range(n)], dtype=np.uint8), 1))
     uniq = {}
     for m, fm in out:
         uniq[(bytes(bytearray(m)), fm)] = (m, fm)

@@ -207,7 +207,8 @@ class FusedAWGN(nn.Module):
     keyed by `seed`.  A draw is keyed by (SNR point, iteration): forward / llrs / error_counts take
     stream=(point, iteration) (sim_ber passes its loop indices, so a speculatively launched
     iteration never shifts another point's codewords); without it every call draws the next
-    iteration of point 0 (`iteration` counts those calls).  Stream row r of a draw is codeword
+    iteration of point 0 (`iteration` counts those calls).  The key is `seed` in the first run and
+    changes with every run sim_ber makes over the model (`epoch`, next_epoch()).  Stream row r of a draw is codeword
     row0 + r; the point lives in the row's high 32 bits (counter word 1), so row0 + batch_size
     must stay below 2^32.  `row0` offsets the rows (a rank's shard of a multi-GPU batch)."""
 
@@ -225,12 +226,24 @@ class FusedAWGN(nn.Module):
         self.decoder = decoder
         self.cw_estimates = cw_estimates
         self.seed, self.row0, self.iteration = int(seed), int(row0), 0
+        self.epoch = 0  # runs of sim_ber over this model so far (next_epoch): part of the Philox key
         if not 0 <= self.row0 < 2 ** 32:
             raise ValueError(f"row0 must be in [0, 2^32), got {row0}")
         self._mask = frozen_mask(frozen_pos, self.n)
         assert self.n - int(self._mask.sum()) == self.k, "k must equal n - len(frozen_pos)"
         self.device = tc.device(device) if device is not None else tc.device("cuda", tc.cuda.current_device())
         self._plans = _lib.PlanSet()
+
+    def next_epoch(self):
+        """Start a new run: the following draws use a fresh Philox key (sim_ber calls this once
+        per run, so repeating a sweep over the same model does not repeat its codewords; the
+        reference draws them from its advancing global RNG)."""
+        self.epoch += 1
+
+    def key(self):
+        """The Philox key of the current epoch: the seed itself in epoch 0, otherwise the seed
+        XOR a Weyl multiple of the epoch (distinct keys for distinct epochs of one seed)."""
+        return (self.seed ^ (self.epoch * 0x9E3779B97F4A7C15)) & (2 ** 64 - 1)
 
     def _make_plan(self, dev):
         from . import _lib
@@ -256,7 +269,7 @@ class FusedAWGN(nn.Module):
         no = float(ebnodb2no(float(ebno_db), self.n_bits_per_sym, self.coderate))
         it, row0 = self._draw(batch_size, stream)
         bits, llr = ops.awgn_qpsk_llr(self._plans.get(self.device, self._make_plan), int(batch_size), no,
-                                      self.seed, it, row0)
+                                      self.key(), it, row0)
         return bits, None, llr
 
     def forward(self, batch_size, ebno_db, stream=None):
@@ -291,13 +304,13 @@ class FusedAWGN(nn.Module):
         it, row0 = self._draw(batch_size, stream)
         if self.sim_kernel:
             try:
-                return ops.sc_sim_count(plan, int(batch_size), no, self.seed, it, row0, counts)
+                return ops.sc_sim_count(plan, int(batch_size), no, self.key(), it, row0, counts)
             except _lib.PolarLibError as e:
                 if e.code != _lib.PL_ENOTSUP:
                     raise
                 self.sim_kernel = False  # this plan's kernel has no fused entry: the two-kernel path
         ubits, llr = ops.awgn_qpsk_llr_bits(self._plans.get(self.device, self._make_plan), int(batch_size), no,
-                                            self.seed, it, row0)
+                                            self.key(), it, row0)
         return ops.sc_decode_count(plan, llr, ubits, counts)
 
 

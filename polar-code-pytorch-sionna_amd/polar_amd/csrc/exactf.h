@@ -12,7 +12,8 @@
 //
 // exp_cr / log_cr evaluate in fp64 over the range f uses and round once to fp32; their fp64
 // error (< 2^-50 relative) leaves a wrong fp32 rounding only for arguments within 2^-26 ulp of a
-// rounding boundary.  Range: exp_cr for |x| <= 87 (normal fp32 results), log_cr for finite x > 0.
+// rounding boundary.  Range: exp_cr for |x| <= 87 (normal fp32 results), log_cr for finite x > 0;
+// plans with llr_max > 43 take the full-range forms (exp_cr_wide / log_cr_wide) instead.
 #pragma once
 #ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
@@ -78,10 +79,40 @@ __device__ __forceinline__ float log_cr(float xf) {
     return (float)__builtin_fma(de, kLn2Hi, __builtin_fma(de, kLn2Lo, lm));
 }
 
+// Full-range forms, for plans whose llr_max exceeds 43 (then xc + yc can leave exp_cr's range):
+// exp rounds p 2^k once in the fp64 -> fp32 conversion (overflow to +inf and subnormal results
+// correctly rounded, as torch's expf), log maps +inf to +inf and 0 to -inf (torch's logf), so
+// f follows the reference through overflow (inf, or inf - inf = NaN, as the reference's own).
+__device__ __forceinline__ float exp_cr_wide(float xf) {
+    const double x = (double)__builtin_amdgcn_fmed3f(xf, -200.0f, 200.0f);  // e^+-200: inf / 0 in fp32
+    constexpr double kLog2e = 1.4426950408889634;
+    constexpr double kLn2Hi = 0x1.62e42fefa39efp-1, kLn2Lo = 0x1.abc9e3b39803fp-56;
+    const double k = __builtin_rint(x * kLog2e);
+    double r = __builtin_fma(-k, kLn2Hi, x);
+    r = __builtin_fma(-k, kLn2Lo, r);
+    double p = kExpC[10];
+#pragma unroll
+    for (int i = 9; i >= 0; --i) p = __builtin_fma(p, r, kExpC[i]);
+    return (float)__builtin_ldexp(p, (int)k);  // exact scaling in fp64, one rounding to fp32
+}
+__device__ __forceinline__ float log_cr_wide(float xf) {
+    const float r = log_cr(xf);
+    return xf == __builtin_inff() ? xf : xf == 0.0f ? -__builtin_inff() : r;
+}
+__device__ __attribute__((noinline)) float f_exact_wide(float x, float y, float lmax) {
+    const float xc = fminf(fmaxf(x, -lmax), lmax), yc = fminf(fmaxf(y, -lmax), lmax);
+    float o = log_cr_wide(1.0f + exp_cr_wide(xc + yc));
+    o -= log_cr_wide(exp_cr_wide(xc) + exp_cr_wide(yc));
+    return o;
+}
+// exp_cr's range |x| <= 87 holds for every argument f forms when llr_max <= 43 (|xc + yc| <= 86)
+constexpr float kExactFastLmax = 43.0f;
+
 // f of my_sn/fec/polar/dec.py:39-43 on clipped inputs, each operation rounded as the reference does.
 // Out of line: inlined into the fully unrolled specialised SC kernels (hundreds of f per lane) the
 // fp64 code made one (128,256) kernel take minutes to compile.
 __device__ __attribute__((noinline)) float f_exact(float x, float y, float lmax) {
+    if (lmax > kExactFastLmax) return f_exact_wide(x, y, lmax);
     const float xc = fminf(fmaxf(x, -lmax), lmax), yc = fminf(fmaxf(y, -lmax), lmax);
     float o = log_cr(1.0f + exp_cr(xc + yc));
     o -= log_cr(exp_cr(xc) + exp_cr(yc));
@@ -95,6 +126,7 @@ struct f2 {
     float a, b;
 };
 __device__ __attribute__((noinline)) f2 f_exact2(float x0, float y0, float x1, float y1, float lmax) {
+    if (lmax > kExactFastLmax) return f2{f_exact_wide(x0, y0, lmax), f_exact_wide(x1, y1, lmax)};
     const float xc0 = fminf(fmaxf(x0, -lmax), lmax), yc0 = fminf(fmaxf(y0, -lmax), lmax);
     const float xc1 = fminf(fmaxf(x1, -lmax), lmax), yc1 = fminf(fmaxf(y1, -lmax), lmax);
     const float s0 = exp_cr(xc0 + yc0), s1 = exp_cr(xc1 + yc1);

@@ -89,6 +89,13 @@ __device__ __forceinline__ double f_ms(double x, double y, double lmax) {  // po
     const bool neg = (__double_as_longlong(x) ^ __double_as_longlong(y)) < 0;
     return neg ? -m : m;
 }
+// Diagnostic macros (timing ablations with WRONG results) exist only in development builds.
+#ifndef PL_DEV
+#define PL_DEV 0
+#endif
+#if !PL_DEV && defined(PL_SCL_DIAG_FMS_ALL) && PL_SCL_DIAG_FMS_ALL
+#error "PL_SCL_DIAG_FMS_ALL gives wrong results: development builds (-DPL_DEV=1) only"
+#endif
 #ifndef PL_SCL_FEX_FORM
 #define PL_SCL_FEX_FORM 1  // exact f: 1 = softplus.h f_exact_pm (no cancellation), 0 = the reference's expression (ocml)
 #endif

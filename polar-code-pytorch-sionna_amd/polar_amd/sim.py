@@ -72,7 +72,10 @@ def sim_ber(mc_fun, ebno_dbs, batch_size, max_mc_iter, soft_estimates=False, tar
     With process_group set, each rank simulates its own batch_size codewords per iteration and the
     counters are summed over ranks (global BER/BLER); the return values are identical on all ranks.
     max_window: iterations per host read for keyed models (default MAX_WINDOW; 1 = the reference's
-    read after every iteration).  return_counts adds the int64 [points, 4] counters
+    read after every iteration).  The counter block is all-reduced on the group backend's device
+    (an RCCL group: the model's GPU; gloo: the host), whatever `device` says.  A model with
+    next_epoch() (channel.FusedAWGN) is advanced once per call, so a second run over the same
+    model draws fresh codewords, as the reference's global RNG would.  return_counts adds the int64 [points, 4] counters
     [bit errors, block errors, bits, blocks]."""
     dist = None
     if process_group is not None:
@@ -81,8 +84,8 @@ def sim_ber(mc_fun, ebno_dbs, batch_size, max_mc_iter, soft_estimates=False, tar
     verbose = verbose and rank0
     ebno_dbs = tc.from_numpy(np.asarray(ebno_dbs)).to(tc.float32)
     P = ebno_dbs.shape[0]
-    cdev = tc.device(device)
     model = _model_of(mc_fun)
+    cdev = _counter_device(device, dist, process_group, model)
     keyed = bool(getattr(model, "keyed_streams", False))
     wmax = (MAX_WINDOW if max_window is None else max(1, int(max_window))) if keyed else 1
     # channel.FusedAWGN with this package's SC decoder: decode and count in one kernel, no bit rows
@@ -130,6 +133,10 @@ def sim_ber(mc_fun, ebno_dbs, batch_size, max_mc_iter, soft_estimates=False, tar
             if verbose:
                 print(f"\nSimu stopped as no error occurred @ EbNo = {ebno_dbs[i].numpy():.1f} dB.\n")
             break
+    # the next run draws fresh codewords (keyed models: a new epoch of the (point, iteration) key)
+    next_epoch = getattr(model, "next_epoch", None)
+    if callable(next_epoch):
+        next_epoch()
     c = tc.from_numpy(cnt)
     ber = c[:, 0] / c[:, 2]
     bler = c[:, 1] / c[:, 3]
@@ -138,6 +145,20 @@ def sim_ber(mc_fun, ebno_dbs, batch_size, max_mc_iter, soft_estimates=False, tar
     if return_counts:
         return ber, bler, c
     return ber, bler
+
+
+def _counter_device(device, dist, process_group, model):
+    """Where the per-window counter block is reduced: an RCCL ("nccl") group reduces device
+    tensors, so the block goes to the model's GPU (else the current one) whatever `device` says;
+    gloo and other CPU backends reduce host tensors; without a group, `device` as given."""
+    if dist is None:
+        return tc.device(device)
+    if dist.get_backend(process_group) == "nccl":
+        mdev = getattr(model, "device", None)
+        if mdev is not None and tc.device(mdev).type == "cuda":
+            return tc.device(mdev)
+        return tc.device("cuda", tc.cuda.current_device())
+    return tc.device("cpu")
 
 
 def _run_window(mc_fun, model, fused, keyed, point, it0, w, batch_size, ebno, soft_estimates):

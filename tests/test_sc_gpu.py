@@ -198,6 +198,30 @@ def test_sc_exact_mode_statistical(pa, kind):
     assert rows >= 2000 and binom_upper_ok(mism, rows, 1e-4), (mism, rows)
 
 
+@pytest.mark.parametrize("kind", KINDS)
+def test_sc_exact_large_llr_max_overflows_like_the_reference(pa, kind):
+    """Exact-f SC plans with llr_max > 43: xc + yc then leaves exp's finite range,
+    log(1 + exp(xc + yc)) must be +inf as in torch (log(inf) = inf), not NaN, and the decisions
+    follow.  n = 2 and 4, every frozen pattern: there g never adds two infinities of opposite
+    sign, so neither decoder reaches a NaN and the oracle (glibc expf/logf, same llr_max) is
+    exact.  Inputs of magnitude 30-60 at llr_max = 60 (and 100): most f overflow."""
+    from polar_amd import _lib
+    g = np.random.default_rng(7)
+    for lmax in (60.0, 100.0):
+        for n in (2, 4):
+            x = (g.uniform(30.0, 60.0, (512, n)) * g.choice([-1.0, 1.0], (512, n))).astype(np.float32)
+            x[:16] = np.float32(lmax) * np.sign(x[:16])  # saturated rows
+            for code in range(1, 1 << n):  # k >= 1
+                mask = np.array([(code >> i) & 1 for i in range(n)], dtype=np.uint8) ^ 1
+                fp = np.flatnonzero(mask)
+                flags = _lib.PL_PLAN_GENERIC if kind == "generic" else _lib.PL_PLAN_CACHE_ONLY
+                plan = _lib.Plan(n, mask, 1, _lib.PL_F_EXACT, lmax, flags=flags)
+                assert plan.kernel()[0] == kind, plan.kernel()
+                got = pa.ops.sc_decode(plan, torch.from_numpy(x).cuda()).cpu().numpy()
+                want = oracle.sc_decode(x, fp, f_mode=1, llr_max=lmax)
+                assert np.array_equal(got, want), (lmax, n, code, int((got != want).any(1).sum()))
+
+
 def test_sc_specialized_jit_for_an_arbitrary_code(pa, tmp_path, monkeypatch):
     """A code with no pre-built kernel: compiled by hiprtc at plan creation, cached, bit-exact."""
     from polar_amd import _lib

@@ -143,3 +143,56 @@ def test_fused_awgn_stream_keys():
         m._draw(2 ** 32, (0, 0))
     with pytest.raises(ValueError):
         channel.FusedAWGN(64, 32, fp, None, device="cpu", row0=2 ** 32)
+
+
+def test_fused_awgn_epochs_rekey_each_run():
+    """sim_ber advances a keyed model's epoch once per run, so running the same sweep
+    twice over one FusedAWGN draws fresh codewords; epoch 0 keeps the seed itself (the pinned
+    streams of the GPU tests)."""
+    from polar_amd import channel, frozen, sim
+
+    class Keyed(channel.FusedAWGN):
+        keys = []
+
+        def error_counts(self, batch_size, ebno_db, counts=None, stream=None):
+            return None  # no fused path: sim_ber calls forward()
+
+        def forward(self, batch_size, ebno_db, stream=None):
+            self.keys.append((self.key(), stream))
+            b = tc.zeros((batch_size, self.k))
+            return b, b
+
+    fp = frozen.reference_frozen_pos(32, 64)
+    m = Keyed(64, 32, fp, None, device="cpu", seed=42)
+    assert m.key() == 42
+    sim.sim_ber(m, [1.0], 4, max_mc_iter=2, verbose=False)
+    sim.sim_ber(m, [1.0], 4, max_mc_iter=2, verbose=False)
+    k1 = {k for k, _ in Keyed.keys[:2]}
+    k2 = {k for k, _ in Keyed.keys[2:]}
+    assert k1 == {42} and len(k2) == 1 and k2 != k1 and m.epoch == 2
+    assert [s for _, s in Keyed.keys[:2]] == [s for _, s in Keyed.keys[2:]]  # same (point, iteration) streams
+    keys = set()
+    for _ in range(100):
+        keys.add(m.key())
+        m.next_epoch()
+    assert len(keys) == 100
+
+
+def test_counter_device_follows_the_group_backend():
+    """an RCCL group reduces device tensors, so the counter block goes to the
+    model's GPU (or the current one) whatever `device` says; gloo reduces on the host."""
+    from polar_amd import sim
+
+    class FakeDist:
+        def __init__(self, backend):
+            self.backend = backend
+
+        def get_backend(self, group=None):
+            return self.backend
+
+    class M:
+        device = tc.device("cuda", 3)
+
+    assert sim._counter_device("cpu", None, None, M()) == tc.device("cpu")
+    assert sim._counter_device("cpu", FakeDist("nccl"), None, M()) == tc.device("cuda", 3)
+    assert sim._counter_device("cuda", FakeDist("gloo"), None, M()) == tc.device("cpu")
