@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sim-iteration", action="store_true",
                     help="skip the (untimed-region) Monte-Carlo iteration measurement of the fused producer")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the (untimed-region) lines of BASELINE.json configs[1] and configs[3]")
     a = ap.parse_args()
     if a.bs is None:
         a.bs = 65536 if a.decoder == "sc" else 8192  # BASELINE.json configs[2] / configs[3]
@@ -203,6 +205,77 @@ def sim_iteration(plan, fp, k, n, bs, ebno, dev, reps=20):
     return res
 
 
+def _time_launches(fn, steps, warmup, settle_ms, dev):
+    """Average ms per call of fn() over `steps` back-to-back calls on the current stream (HIP
+    events on that stream), after ~settle_ms of untimed calls (DVFS) and `warmup` more."""
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < settle_ms:
+        for _ in range(20):
+            fn()
+        torch.cuda.synchronize(dev)
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize(dev)
+    stream = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    return e0.elapsed_time(e1) / steps
+
+
+def config_line(decoder, k, n, bs, L, ebno, dev, rank, steps, warmup):
+    """One more BASELINE.json configuration on this GPU, measured after the headline's timed
+    region: kernel ms per launch (HIP events over back-to-back launches on one resident batch),
+    Mcodewords/s, info Gbit/s, BLER, and the HBM roofline of the launch (bs (4n + 4k) bytes)."""
+    import polar_amd
+    from polar_amd import _lib, channel, ops
+    fp = polar_amd.reference_frozen_pos(k, n)
+    plan = _lib.Plan(n, polar_amd.frozen_mask(fp, n), L, _lib.PL_F_MINSUM, device=dev)
+    gen = torch.Generator(device=dev).manual_seed(1042 + rank)
+    model = channel.System_AWGN_model(n, k, channel.GpuEncoder(fp, n), None, device=dev, generator=gen)
+    with torch.no_grad():
+        bits, _, llr = model.llrs(bs, torch.tensor(ebno, dtype=torch.float32))
+    llr = llr.contiguous()
+    out = torch.empty((bs, k), dtype=torch.float32, device=dev)
+    ws = ops.scl_workspace(plan, bs, dev) if L > 1 else None
+    if L > 1:
+        fn = lambda: ops.scl_decode(plan, llr, out=out, workspace=ws)  # noqa: E731
+    else:
+        fn = lambda: ops.sc_decode(plan, llr, out=out)  # noqa: E731
+    ms = _time_launches(fn, steps, warmup, 50.0, dev)
+    nerr = int(torch.any(out != bits, dim=-1).sum().item())
+    nbytes = bs * (4 * n + 4 * k)
+    ach = nbytes / (ms * 1e-3) / 1e9
+    res = {"workload": f"{'SCL' if L > 1 else 'SC'} decode (k={k}, n={n}), bs={bs}" + (f", L={L}" if L > 1 else ""),
+           "kernel": plan.kernel()[0], "kernel_ms": round(ms, 5), "steps": steps,
+           "mcw_s": round(bs / ms / 1e3, 3), "info_gbit_s": round(bs * k / ms / 1e6, 4),
+           "dtype": "f64" if L > 1 else "f32", "bler": round(nerr / bs, 6),
+           "roofline_hbm": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(ach / HBM_PEAK_GBS, 5), "algorithmic_bytes_per_launch": nbytes}}
+    return res, fn, plan, llr, out
+
+
+def latency_roofline(plan, llr, k, n, bs, ms_full, dev, steps=400):
+    """Latency bound of a batch that fills less than one wave per SIMD: the same launch with one
+    wave of codewords (64 / G of them, G = lanes per codeword of the specialised min-sum kernel:
+    n/64 for n = 256 ... 1024, else max(1, n/128)) -- the dependent chain of one wave on an idle
+    chip, launch included -- against the full batch's launch time.  frac = single-wave time / full
+    time (1.0 = the batch costs no more than its critical path)."""
+    from polar_amd import ops
+    g = n // 64 if 256 <= n <= 1024 else max(1, n // 128)
+    cpw = 64 // g
+    one = llr[:cpw].contiguous()
+    out1 = torch.empty((cpw, k), dtype=torch.float32, device=dev)
+    t1 = _time_launches(lambda: ops.sc_decode(plan, one, out=out1), steps, 20, 20.0, dev)
+    return {"bound": "latency", "single_wave_ms": round(t1, 5), "codewords_per_wave": cpw,
+            "waves": -(-bs // cpw), "achieved_ms": round(ms_full, 5), "frac": round(t1 / ms_full, 4),
+            "note": "one wave of codewords per launch (its dependent chain, on an idle chip) vs the whole "
+                    "batch; the batch fills fewer waves than the chip's 1024 SIMDs"}
+
+
 def plan_mask(fp, n):
     import polar_amd
     return polar_amd.frozen_mask(fp, n)
@@ -347,6 +420,17 @@ def main():
     sim_it = None
     if a.decoder == "sc" and not a.no_sim_iteration:
         sim_it = sim_iteration(plan, fp, k, n, bs, a.ebno, dev)
+    configs = None
+    if a.decoder == "sc" and not a.no_configs and (k, n, bs) == (512, 1024, 65536):
+        # BASELINE.json configs[1] (k=128, n=256, bs=4096, SC) and configs[3] (k=512, n=1024,
+        # L=8, bs=8192, SCL) on this GPU, after the headline's timed region
+        c1, _, p1, l1, _ = config_line("sc", 128, 256, 4096, 1, a.ebno, dev, rank, 2000, 200)
+        c1["roofline_latency"] = latency_roofline(p1, l1, 128, 256, 4096, c1["kernel_ms"], dev)
+        c3, _, _, _, _ = config_line("scl", 512, 1024, 8192, 8, a.ebno, dev, rank, 20, 3)
+        rv = valu_roofline("scl_k512_n1024_bs8192_L8", c3["kernel_ms"])
+        if rv is not None:
+            c3["roofline_valu"] = rv
+        configs = {"configs_1": c1, "configs_3": c3}
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(llr.cpu().numpy(), fp.numpy(), k, n, a.decoder, L, a.cpu_seconds)
@@ -387,6 +471,8 @@ def main():
             line["roofline_valu"] = rv
         if sim_it is not None:
             line["sim_iteration"] = sim_it
+        if configs is not None:
+            line.update(configs)
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
