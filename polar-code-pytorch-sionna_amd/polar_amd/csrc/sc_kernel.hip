@@ -632,6 +632,7 @@ __global__ __launch_bounds__(64 * kWavesPerBlock, PL_SC_MIN_WAVES) void sc_decod
     c.lane = lane;
     c.lig = lane & (G - 1);
     c.lmax = lmax;
+    if constexpr (FM == 1) plx::load_tables(threadIdx.x, blockDim.x);  // the exact f's exp / log tables
 
     uint64_t lo, hi;
     root<LOG_N, LOG_G, FM>(ch, c, lo, hi);

@@ -240,6 +240,9 @@ __device__ __forceinline__ float fop(float x, float y, float lmax) {
 #ifndef PL_SC_FEX_PAIR
 #define PL_SC_FEX_PAIR 1
 #endif
+#ifndef PL_SC_FEX_LANE
+#define PL_SC_FEX_LANE 1  // exact f of lane-level nodes split over the lanes holding the pair (f_lane_exact)
+#endif
 template <int FM, bool BND, int H>
 __device__ __forceinline__ void fvec(const float* a, float* x, float lmax) {
     if constexpr (FM == 1 && H >= 2 && PL_SC_FEX_PAIR) {
@@ -348,12 +351,60 @@ __device__ __forceinline__ bool multi_in_block(uint64_t m, uint64_t live) {
 template <class C, int s, int P>
 __device__ uint32_t lnode(float a, const Lane& ln);
 
+// Exact f of a lane-level node (FM = 1), the transcendentals split over the lanes that hold the
+// same pair.  At a node of size S <= G lane q pairs with q ^ (S-1); below the top lane level
+// (S < G) lane q ^ (2S-1) holds a copy of lane q's value (its parent's f / g is symmetric), so
+// four lanes evaluate the same f: the low half of each 2S-lane block (role A) takes
+// log(1 + exp(x + y)), the high half (role B) log(exp(x) + exp(y)) -- each lane one exp of its
+// own argument, the pair's sum e^x + e^y by one mirror DPP, one log -- and the halves swap their
+// logs with one more mirror.  At S = G only the two lanes of the pair share the f: both take
+// exp of their own value and of x + y, then one log each (role A: the lane holding the pair's
+// low element).  Every lane ends with the same bits as f_exact(x, y) -- each sum is commutative,
+// each transcendental correctly rounded -- so the replication the layout relies on holds.
+// 1 exp + 1 log per lane (S < G) or 2 + 1 (S = G) instead of 3 + 2.
+template <int S, bool TOP>
+__device__ __attribute__((noinline)) float f_lane_exact(float a, float y, uint32_t role31, float lmax) {
+    if (lmax > plx::kExactFastLmax) return plx::f_exact_wide(a, y, lmax);
+    const float xc = fminf(fmaxf(a, -lmax), lmax), yc = fminf(fmaxf(y, -lmax), lmax);
+    const bool A = (int32_t)role31 < 0;
+    float arg;
+    if constexpr (TOP) {
+        const float e = plx::exp_cr(xc);
+        const float es = e + mirf<S>(e);  // e^x + e^y in both lanes of the pair
+        const float e1 = plx::exp_cr(xc + yc);
+        arg = A ? 1.0f + e1 : es;
+    } else {
+        const float e = plx::exp_cr(A ? xc + yc : xc);
+        const float es = e + mirf<S>(e);  // role B: e^x + e^y (its partner is role B too)
+        arg = A ? 1.0f + e : es;
+    }
+    const float l = plx::log_cr(arg);
+    float lo;  // the other role's log
+    if constexpr (TOP) lo = mirf<S>(l);
+    else lo = mirf<2 * S>(l);
+    return A ? l - lo : lo - l;
+}
+
 template <class C, int s, int P>
 __device__ __forceinline__ uint32_t lsplit(float a, const Lane& ln) {
     constexpr int S = 1 << s;
     const float y = mirf<S>(a);
     uint32_t bl = 0;
-    if constexpr (nt<C>(s - 1, P) != R0) bl = lnode<C, s - 1, P>(fop<C::FM, lchild<C>(s, P)>(a, y, ln.lmax), ln);
+    if constexpr (nt<C>(s - 1, P) != R0) {
+        float x;
+        if constexpr (C::FM == 1 && PL_SC_FEX_LANE) {
+            // role bit: the pair's low element (S = G), the low half of the 2S-block (S < G)
+#if PL_SC_LANE31
+            const uint32_t role = s == C::LOG_G ? ln.lo31[s] : ln.lo31[s + 1];
+#else
+            const uint32_t role = s == C::LOG_G ? ln.lom(s) : ln.lom(s + 1);
+#endif
+            x = f_lane_exact<S, s == C::LOG_G>(a, y, role, ln.lmax);
+        } else {
+            x = fop<C::FM, lchild<C>(s, P)>(a, y, ln.lmax);
+        }
+        bl = lnode<C, s - 1, P>(x, ln);
+    }
 #if PL_SC_LANE31
     // both lanes of the pair evaluate (1-2u) alpha_lo + alpha_hi: the low lane flips its own
     // value (bitop3 S1 ^ (S0 & S2) with the lane's bit-31 mask), the high lane keeps its own, and
@@ -665,7 +716,15 @@ __device__ __forceinline__ float valpha(const float (&ch)[C::NS], int side, uint
 template <class C, int SIDE>
 __device__ __forceinline__ void valphas(const float (&ch)[C::NS], uint64_t blr, float (&a)[C::NS / 2], float lmax) {
     constexpr int E = C::NS / 2;
-    if constexpr (SIDE == 1 && E >= 2) {
+    if constexpr (SIDE == 0 && C::FM == 1 && E >= 2 && PL_SC_FEX_PAIR) {
+        // exact f on the negated channel (vfroot), two elements per call
+#pragma unroll
+        for (int j = 0; j < E; j += 2) {
+            const plx::f2 r = plx::f_exact2(-ch[j], -ch[j + E], -ch[j + 1], -ch[j + 1 + E], lmax);
+            a[j] = r.a;
+            a[j + 1] = r.b;
+        }
+    } else if constexpr (SIDE == 1 && E >= 2) {
 #pragma unroll
         for (int j = 0; j < E; j += 2) {
             const f2v u = {flip31(ch[j], bit31(blr, j)), flip31(ch[j + 1], bit31(blr, j + 1))};
@@ -1199,6 +1258,7 @@ __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs
     ln.lom_[0] = 0u;
 #endif
     ln.lmax = lmax;
+    if constexpr (C::FM == 1) plx::load_tables(threadIdx.x, blockDim.x);  // the exact f's exp / log tables
     // PL_SC_CH_LDS: each wave's LDS is its channel rows; its u words reuse their first 64 * WPL
     // words once the right half has read them (same wave, LDS in order)
     constexpr int WLDS = Ch<C>::CHL ? (NS / 2) * 64 : 64 * WPL;  // LDS words per wave
@@ -1410,6 +1470,7 @@ __device__ __forceinline__ void decode_staged(const float* __restrict__ llr, int
     ln.lom_[0] = 0u;
 #endif
     ln.lmax = lmax;
+    if constexpr (C::FM == 1) plx::load_tables(threadIdx.x, blockDim.x);
     uint32_t* ubase = lds + wave * 64 * WPL;
     uint32_t* mine = lds + (wave * 64 + lane) * WPL;
     float* rows = reinterpret_cast<float*>(lds + S::U_WORDS) + wave * CW * S::ROW;
