@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sim-iteration", action="store_true",
                     help="skip the (untimed-region) Monte-Carlo iteration measurement of the fused producer")
+    ap.add_argument("--dist", action="store_true",
+                    help="create the process group even at world size 1 (rehearses the RCCL path on one GPU)")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the (untimed-region) lines of BASELINE.json configs[1] and configs[3]")
     a = ap.parse_args()
@@ -334,7 +336,8 @@ def main():
     # one rank per GPU; PL_BENCH_BACKEND=gloo with more ranks than GPUs is the rehearsal of the
     # multi-GPU path on a one-GPU box (ranks share the card, gloo carries the collectives)
     gpu = local % max(torch.cuda.device_count(), 1)
-    if world > 1:
+    backend = None
+    if world > 1 or a.dist:
         import torch.distributed as dist
         torch.cuda.set_device(gpu)
         backend = os.environ.get("PL_BENCH_BACKEND", "nccl")
@@ -404,7 +407,7 @@ def main():
     torch.cuda.synchronize(dev)
     kern_ms = e0.elapsed_time(e1) / a.steps
 
-    cdev = dev if os.environ.get("PL_BENCH_BACKEND", "nccl") == "nccl" else torch.device("cpu")  # gloo: host
+    cdev = dev if backend == "nccl" else torch.device("cpu")  # RCCL reduces device tensors, gloo host ones
     nerr = sum(int(torch.any(o != b, dim=-1).sum().item()) for o, b in zip(outs, bitss))
     blk = torch.tensor([nerr, bs * R], dtype=torch.int64, device=cdev)
     tmax = torch.tensor([wall], dtype=torch.float64, device=cdev)
@@ -460,6 +463,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic_from_profiles(tag),
                          "kernel_ms": round(kern_ms, 5), "algorithmic_bytes_per_launch": bytes_per_launch},
             "cpu_baseline": cpu,
+            "dist_backend": backend,
         }
         rv = valu_roofline(tag, kern_ms)
         if a.decoder == "scl" and rv is not None:

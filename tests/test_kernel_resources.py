@@ -102,3 +102,70 @@ def test_sc_bench_kernel_fits_four_waves_per_simd():
         assert m["vgpr_count"] <= 128, (name, m)  # 4 waves per SIMD (512 VGPRs per lane)
         assert m["vgpr_spill_count"] == 0, (name, m)
         assert m["private_segment_fixed_size"] == 0, (name, m)
+
+
+# ---- instruction-stream pins -------------------------------------------
+# Static instruction counts by class and a hash of the mnemonic sequence of the two bench
+# kernels, as hipcc emits them for gfx950.  A change of either kernel's code shows up here (and
+# must be re-pinned on purpose: python tools/pin_isa.py), so a bench number can always be tied to
+# the instruction stream that produced it; pl_version() carries the source hash on the box.
+PIN_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "kernel_isa.json")
+
+
+def isa_summary(asm, label_pred):
+    """{label: {"valu", "salu", "vmem", "lds", "smem", "dpp", "total", "sha"}} for the functions
+    of `asm` whose label satisfies label_pred (body = label .. its .Lfunc_end)."""
+    import hashlib
+    out = {}
+    lines = asm.split("\n")
+    i = 0
+    while i < len(lines):
+        m = re.match(r"^([A-Za-z_.$][\w.$]*):", lines[i])
+        if m and label_pred(m.group(1)) and not m.group(1).startswith(".L"):
+            name, ops = m.group(1), []
+            i += 1
+            while i < len(lines) and not lines[i].startswith(".Lfunc_end"):
+                t = lines[i].strip().split()
+                if t and re.match(r"^[vsdgb][a-z0-9_]+$", t[0]) and not t[0].startswith("s_nop"):
+                    ops.append(t[0] + ("_dpp" if ("row_" in lines[i] or "quad_perm" in lines[i]) else ""))
+                i += 1
+            c = {"valu": sum(o.startswith("v_") for o in ops), "salu": sum(o.startswith("s_") and not
+                 o.startswith(("s_load", "s_buffer_load", "s_store")) for o in ops),
+                 "vmem": sum(o.startswith(("global_", "buffer_", "scratch_")) for o in ops),
+                 "lds": sum(o.startswith("ds_") for o in ops),
+                 "smem": sum(o.startswith(("s_load", "s_buffer_load")) for o in ops),
+                 "dpp": sum(o.endswith("_dpp") for o in ops), "total": len(ops),
+                 "sha": hashlib.sha256("\n".join(ops).encode()).hexdigest()[:16]}
+            out[name] = c
+        i += 1
+    return out
+
+
+def sc_bench_asm(td):
+    import polar_amd
+    from polar_amd import _lib
+    fp = polar_amd.reference_frozen_pos(512, 1024).numpy()
+    src, _ = _lib.sc_source(1024, polar_amd.frozen_mask(fp, 1024), _lib.PL_F_MINSUM)
+    flags, _ = _lib._source_header(src)
+    extra = [f for f in flags if f not in ("--genco", "--no-gpu-bundle-output", "-O3", "-std=c++17",
+                                           "-ffp-contract=off") and not f.startswith("--offload-arch")]
+    path = os.path.join(td, "sc.hip")
+    with open(path, "w") as f:
+        f.write(src)
+    return _compile_asm(path, extra, td)
+
+
+def current_pins():
+    with tempfile.TemporaryDirectory() as td:
+        sc = isa_summary(sc_bench_asm(td), lambda n: n == "pl_sc_static_f32")
+    scl = isa_summary(_scl_l8_asm(), lambda n: "scl_tree_kernelILi8ELi4ELi0ELb0E" in n)
+    assert len(sc) == 1 and len(scl) == 1, (list(sc), list(scl))
+    return {"sc_k512_n1024_minsum": list(sc.values())[0], "scl_L8_n1024_minsum": list(scl.values())[0]}
+
+
+def test_bench_kernel_instruction_streams_are_pinned():
+    import json
+    want = json.load(open(PIN_PATH))
+    got = current_pins()
+    for key in got:
+        assert got[key] == want[key], (key, got[key], want[key], "re-pin with: python tools/pin_isa.py")

@@ -6,6 +6,10 @@ sim_ber's windowed loop.
     drawing stream rows [r * 65536, (r + 1) * 65536) at (512,1024), Eb/N0 0 ... 4 dB, with a
     block-error target that stops points mid-window: the summed counters are EXACTLY those of
     one rank simulating all 131072 rows (row0 0) -- same codewords, same stop decisions;
+  * configs[4] at its stated size: 8 gloo ranks x 65536 rows = 524288 codewords per iteration,
+    summed counters equal one process over the same rows;
+  * the RCCL backend at world size 1 (device-tensor counter all_reduce in sim_ber; bench.py's
+    barrier / timing max / BLER reduction under torch.distributed.run);
   * the windowed loop equals the one-iteration loop (max_window=1) for the fused SC path and for
     an SCL decoder behind FusedAWGN (forward() + pl_count_errors);
   * the (512,1024) BLER matches the reference's measured table (x_run SC,
@@ -32,28 +36,32 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _sweep(rank, bs, process_group=None, max_window=None):
+def _sweep(rank, bs, process_group=None, max_window=None, target=TARGET):
     import polar_amd
     from polar_amd import channel, sim
     k, n = 512, 1024
     fp = polar_amd.reference_frozen_pos(k, n)
     dec = polar_amd.SC_Dec(fp, n)
     model = channel.FusedAWGN(n, k, fp, dec, device=torch.device("cuda", 0), seed=42, row0=rank * bs)
-    _, _, cnt = sim.sim_ber(model, EBNO, bs, max_mc_iter=4, target_block_errs=TARGET, verbose=False,
+    _, _, cnt = sim.sim_ber(model, EBNO, bs, max_mc_iter=4, target_block_errs=target, verbose=False,
                             device="cpu", process_group=process_group, return_counts=True, max_window=max_window)
     assert model.sim_kernel, "the sweep must run the fused pl_sc_sim_count path"
     return cnt.numpy()
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, backend="gloo", target=TARGET):
     import sys
     sys.path.insert(0, os.path.join(ROOT, "polar-code-pytorch-sionna_amd"))
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group(backend, rank=rank, world_size=world)
     try:
-        cnt = _sweep(rank, BS, process_group=dist.group.WORLD)
+        # device="cpu" on purpose: sim_ber must reduce on the backend's device (RCCL: the GPU)
+        cnt = _sweep(rank, BS, process_group=dist.group.WORLD, target=target)
     finally:
         dist.destroy_process_group()
     np.save(os.path.join(out_dir, f"r{rank}.npy"), cnt)
@@ -70,6 +78,52 @@ def test_two_ranks_one_gpu_equal_one_rank(tmp_path):
     blocks = one[:, 3] // (world * BS)
     assert set(blocks.tolist()) >= {2, 3}, blocks  # points stopped at different iterations
     assert (one[:, 1] >= TARGET).all() or (blocks == 4).any()
+
+
+def test_configs4_eight_ranks_one_gpu_equal_one_rank(tmp_path):
+    """configs[4] at its stated size: 8 ranks x 65536 rows = 524288 codewords per iteration,
+    Eb/N0 0 ... 4 dB, each rank one process on cuda:0 with its shard of the keyed stream (gloo
+    carries the [W, 4] counter all_reduce).  The global counters equal one process decoding all
+    524288 rows per iteration (row0 0): same codewords, same stop decisions."""
+    import torch.multiprocessing as mp
+    world, target = 8, 4 * TARGET
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), "gloo", target), nprocs=world, join=True)
+    r = [np.load(tmp_path / f"r{i}.npy") for i in range(world)]
+    for i in range(1, world):
+        np.testing.assert_array_equal(r[0], r[i])
+    one = _sweep(0, world * BS, target=target)
+    np.testing.assert_array_equal(r[0], one)
+    blocks = one[:, 3] // (world * BS)
+    assert len(set(blocks.tolist())) >= 2, blocks  # points stopped at different iterations
+    assert int(one[0, 3]) >= world * BS
+
+
+def test_rccl_world1_sim_ber_equals_no_group(tmp_path):
+    """The RCCL branch on hardware: one rank, init_process_group("nccl", device_id=cuda:0); sim_ber
+    keeps its [W, 4] counter block on the GPU for the device-tensor all_reduce (sim._counter_device)
+    and returns exactly the counters of the same sweep without a process group."""
+    import torch.multiprocessing as mp
+    mp.spawn(_worker, args=(1, _free_port(), str(tmp_path), "nccl"), nprocs=1, join=True)
+    got = np.load(tmp_path / "r0.npy")
+    np.testing.assert_array_equal(got, _sweep(0, BS))
+
+
+def test_rccl_world1_bench_line(tmp_path):
+    """bench.py under torch.distributed.run with one rank and the RCCL backend (--dist forces the
+    process group at world size 1): barrier, max-over-ranks timing and the BLER counter
+    all_reduce run over RCCL; the JSON line is the single-GPU one."""
+    import json
+    import subprocess
+    import sys
+    env = dict(os.environ, PL_BENCH_BACKEND="nccl")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"), "--dist",
+           "--steps", "50", "--warmup", "5", "--no-cpu-baseline", "--no-sim-iteration", "--no-configs"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 1 and line["config"]["parallelism"] == "dp1" and line["dist_backend"] == "nccl"
+    assert line["value"] > 10.0 and line["bler"] > 0.5
 
 
 def test_window_equals_sequential_fused():
