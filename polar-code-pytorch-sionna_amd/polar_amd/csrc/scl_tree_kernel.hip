@@ -538,9 +538,24 @@ __device__ __forceinline__ void vlev_shared(double* vx, double* vy, double lmax)
     }
 }
 
+// The stage-6 values of the virtual node of 64 (n = 1024, V = 4) that the left pass (f into the
+// stage-5 left child) computes from the channel, per (item, path) of this lane: the right pass (g
+// into the right child) reads them back instead of rebuilding them from the channel.  A path's
+// entry is found through the owner byte sptr[p][6] (written by the left pass, re-pointed with
+// the other stage owners when paths fork), and lives in this lane's private memory: the lane that
+// handles item (c, j) in one pass handles it in every pass.  Half the passes then cost one load
+// and one g per path instead of 31 f/g.
+#ifndef PL_SCL_VCACHE
+#define PL_SCL_VCACHE 1
+#endif
+struct VCache {
+    double2 v[32];  // [it * L + path]: (x, y) = stage-6 elements (j, j + 32); IT * L <= 32
+};
+
 template <int L, int V, int NS, int FM>
 __device__ __forceinline__ void vnode64(const St& t, const Cw& w, const float* cx, const float* cy, const int* wb,
-                                        int j, uint32_t gmask, bool is_g, int pos, int ls) {
+                                        int j, uint32_t gmask, bool is_g, int pos, int ls, VCache* vc = nullptr,
+                                        int it = 0) {
     constexpr int H = 1 << (V - 1);       // values per side after the channel level
     constexpr int K = NS > 0 ? (2 * H) >> NS : 2 * H;  // per side after the shared levels
     double sx[K], sy[K];
@@ -582,16 +597,34 @@ __device__ __forceinline__ void vnode64(const St& t, const Cw& w, const float* c
             vlev_path<V - NS - 1, FM>(vx, vy, bp, wb, j, gmask, t.lmax);
         }
         const double x = vx[0], y = vy[0];
+        if (vc != nullptr) vc->v[it * L + p] = make_double2(x, y);  // the left pass (is_g false)
         const double r = is_g ? g_op(x, y, getbit(bp, pos + j)) : f_op<FM>(x, y, t.lmax);
         w.A[p * t.per + (1 << ls) - (1 << R) + j] = r;
+    }
+}
+// The right pass from the cache: per path, the owner's (x, y) and one g.
+template <int L>
+__device__ __forceinline__ void vnode64_cached(const St& t, const Cw& w, int j, int pos, int ls, const VCache& vc,
+                                               int it) {
+#pragma unroll 1
+    for (int p = 0; p < L; ++p) {
+        const int o = w.sptr[p * SPS + ls + 1];
+        const double2 xy = vc.v[it * L + o];
+        w.A[p * t.per + (1 << ls) - (1 << R) + j] = g_op(xy.x, xy.y, getbit(w.beta + p * t.W, pos + j));
     }
 }
 
 // One pass of a virtual node of 64 over the wave's (codeword, element) pairs; NS leading f
 // levels (a per-pass constant, so each NS is its own loop).
 template <int L, int V, int NS, int FM, int CPW>
-__device__ void vvisit64(const St& t, int pos, bool is_g, int lane, const int* wb, uint32_t gmask) {
+__device__ void vvisit64(const St& t, int pos, bool is_g, int lane, const int* wb, uint32_t gmask, VCache* vc) {
     constexpr int NC = 1 << V, ls = 5, h = 32, hs = 64;
+    if (vc != nullptr && is_g) {
+#pragma unroll 1
+        for (int idx = lane, it = 0; idx < CPW * h; idx += 64, ++it)
+            vnode64_cached<L>(t, t.cw(idx >> ls), idx & (h - 1), pos, ls, *vc, it);
+        return;
+    }
     // channel rows addressed from the wave's first row (uniform base, 32-bit lane offsets)
     const float* ch0 = t.llr + t.b0 * t.n;
 #if PL_SCL_VPF
@@ -632,7 +665,7 @@ __device__ void vvisit64(const St& t, int pos, bool is_g, int lane, const int* w
     }
 #else
 #pragma unroll 1
-    for (int idx = lane; idx < CPW * h; idx += 64) {
+    for (int idx = lane, it = 0; idx < CPW * h; idx += 64, ++it) {
         const int c = idx >> ls, j = idx & (h - 1);
         const Cw w = t.cw(c);
         const int co = (int)(t.b0 + c < t.bs ? c : t.bs - 1 - t.b0) * t.n + j;
@@ -642,7 +675,7 @@ __device__ void vvisit64(const St& t, int pos, bool is_g, int lane, const int* w
             cx[m] = -1.0f * ch0[co + m * hs];
             cy[m] = -1.0f * ch0[co + h + m * hs];
         }
-        vnode64<L, V, NS, FM>(t, w, cx, cy, wb, j, gmask, is_g, pos, ls);
+        vnode64<L, V, NS, FM>(t, w, cx, cy, wb, j, gmask, is_g, pos, ls, vc, it);
     }
 #endif
 }
@@ -909,7 +942,7 @@ __device__ __forceinline__ void node_fg_st(const St& t, int pos, bool is_g, int 
 }
 
 template <int L, int V, int FM, int CPW>
-__device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane) {
+__device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane, VCache* vc) {
     constexpr int LL = ilog2(L);
     const int ls = s - 1, h = 1 << ls;
     if (PL_SCL_DIAG_SKIP_V && s > t.SS) {
@@ -968,11 +1001,11 @@ __device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane) {
             // leading f levels from the channel down: path-independent
             const int ns = (gmask & 8u) ? 0 : (gmask & 4u) ? 1 : (gmask & 2u) ? 2 : (gmask & 1u) ? 3 : 4;
             switch (ns) {
-                case 0: vvisit64<L, V, 0, FM, CPW>(t, pos, is_g, lane, wb, gmask); break;
-                case 1: vvisit64<L, V, 1, FM, CPW>(t, pos, is_g, lane, wb, gmask); break;
-                case 2: vvisit64<L, V, 2, FM, CPW>(t, pos, is_g, lane, wb, gmask); break;
-                case 3: vvisit64<L, V, 3, FM, CPW>(t, pos, is_g, lane, wb, gmask); break;
-                default: vvisit64<L, V, 4, FM, CPW>(t, pos, is_g, lane, wb, gmask); break;
+                case 0: vvisit64<L, V, 0, FM, CPW>(t, pos, is_g, lane, wb, gmask, vc); break;
+                case 1: vvisit64<L, V, 1, FM, CPW>(t, pos, is_g, lane, wb, gmask, vc); break;
+                case 2: vvisit64<L, V, 2, FM, CPW>(t, pos, is_g, lane, wb, gmask, vc); break;
+                case 3: vvisit64<L, V, 3, FM, CPW>(t, pos, is_g, lane, wb, gmask, vc); break;
+                default: vvisit64<L, V, 4, FM, CPW>(t, pos, is_g, lane, wb, gmask, vc); break;
             }
         } else if constexpr (FM == 1 && V >= 1 && PL_SCL_FEX_HOIST) {
             vvisit_ex<L, V, CPW>(t.llr, t.b0, t.bs, t.n, t.W, t.per, t.lmax, t.smem, t.y.bytes, t.y.off_A,
@@ -1018,7 +1051,12 @@ __device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane) {
         }
         }
     }
-    if (lane < CPW * L) t.cw(lane >> LL).sptr[(lane & (L - 1)) * SPS + ls] = (uint8_t)(lane & (L - 1));
+    if (lane < CPW * L) {
+        uint8_t* sp = t.cw(lane >> LL).sptr + (lane & (L - 1)) * SPS;
+        sp[ls] = (uint8_t)(lane & (L - 1));
+        // the left pass of a cached virtual node: each path now owns its own stage-6 cache entry
+        if (vc != nullptr && !is_g && s > t.SS) sp[s] = (uint8_t)(lane & (L - 1));
+    }
     __syncthreads();
 }
 
@@ -1719,6 +1757,8 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
         }
     }
 
+    VCache vcache_lane;  // min-sum, n = 1024 (V = 4): the virtual node-of-64 cache (vnode64)
+    VCache* vcp = (PL_SCL_VCACHE && !PL_SCL_VPF && FM == 0 && V == 4) ? &vcache_lane : nullptr;
     double pm = gl == 0 || gl == L ? 0.0 : lmax;  // :192-194 ([0, 30 x (L-1)] per half)
     const int nsub = n >> R;
     int q = 0;
@@ -1733,7 +1773,7 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
         } else {
             const int tz = __builtin_ctz(i0);
             if (!PL_SCL_DIAG_NO_UPPER && tz <= t.SS)
-                node_fg<L, V, FM, CPW>(t, tz + 1, i0 & ~((2 << tz) - 1), true, lane);
+                node_fg<L, V, FM, CPW>(t, tz + 1, i0 & ~((2 << tz) - 1), true, lane, vcp);
             top = tz;
         }
         int pr = 0, kind = 0;
@@ -1745,7 +1785,7 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
                     break;
                 }
             }
-            if (!PL_SCL_DIAG_NO_UPPER && s > R && s - 1 <= t.SS) node_fg<L, V, FM, CPW>(t, s, i0, false, lane);
+            if (!PL_SCL_DIAG_NO_UPPER && s > R && s - 1 <= t.SS) node_fg<L, V, FM, CPW>(t, s, i0, false, lane, vcp);
         }
         if (FAST && kind != 0) {
             upper_prune<L, V, FM, CPW>(t, pr, i0, kind, pm, lane);

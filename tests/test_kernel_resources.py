@@ -64,7 +64,9 @@ def test_scl_bench_kernel_has_no_spills_or_scratch():
     assert len(meta) == 1, list(meta)
     (m,) = meta.values()
     assert m["vgpr_spill_count"] == 0, m
-    assert m["private_segment_fixed_size"] == 0, m
+    # private memory: only the per-lane virtual node-of-64 cache (VCache, 512 B; round 4, A/B
+    # 0.925 vs 0.978 ms) and the 16-byte frame -- no register spills
+    assert m["private_segment_fixed_size"] <= 528, m
     assert m["vgpr_count"] <= 256, m  # amdgpu_waves_per_eu(2)
 
 
