@@ -708,7 +708,8 @@ __device__ void vvisit64(const St& t, int pos, bool is_g, int lane, const int* w
 template <int L, int V, int CPW>
 __device__ PL_FEX_PASS_ATTR void vvisit_ex(const float* __restrict__ llr, int64_t b0, int64_t bs, int n, int W, int per,
                                        double lmax, unsigned char* smem, int cw_bytes, int off_A, int off_beta,
-                                       int s, int pos, int is_g, int lane, const double* __restrict__ vcache) {
+                                       int s, int pos, int is_g, int lane, const double* __restrict__ vcache,
+                                       VCache* vc = nullptr, int off_sptr = 0) {
     // Out of line with scalar arguments only: the pass's register arrays are allocated apart from
     // the lane subtree's state (inlined, the two together spilled), and nothing goes through
     // scratch but the call's own register saves, once per pass.
@@ -737,11 +738,20 @@ __device__ PL_FEX_PASS_ATTR void vvisit_ex(const float* __restrict__ llr, int64_
     const bool combo = PL_SCL_FEX_COMBO && ns < V && q1 >= 1 && ((gmask >> (q1 - 1)) & 1u) == 0u;
     typedef double wv __attribute__((ext_vector_type(NC)));
 #pragma unroll 1
-    for (int idx = lane; idx < CPW * h; idx += 64) {
+    for (int idx = lane, it = 0; idx < CPW * h; idx += 64, ++it) {
         const int c = idx >> ls, j = idx & (h - 1);
         unsigned char* base = smem + c * cw_bytes;
         double* A = reinterpret_cast<double*>(base + off_A);
         const uint32_t* beta = reinterpret_cast<const uint32_t*>(base + off_beta);
+        if (vc != nullptr && is_g) {  // the right pass from the left pass's values (VCache)
+            const uint8_t* sptr = base + off_sptr;
+#pragma unroll 1
+            for (int p = 0; p < L; ++p) {
+                const double2 xy = vc->v[it * L + sptr[p * SPS + s]];
+                A[p * per + (1 << ls) - (1 << R) + j] = g_op(xy.x, xy.y, getbit(beta + p * W, pos + j));
+            }
+            continue;
+        }
         const int co = (int)(b0 + c < bs ? c : bs - 1 - b0) * n + j;
         // One register block per side holds what the path loop reads: the channel elements
         // j + m 2^s (x; y: + 2^(s-1)) as doubles when the channel level is per path (ns = 0), the
@@ -888,6 +898,7 @@ __device__ PL_FEX_PASS_ATTR void vvisit_ex(const float* __restrict__ llr, int64_
                 }
             }
             const double x = vx[0], y = vy[0];
+            if (vc != nullptr) vc->v[it * L + p] = make_double2(x, y);  // the left pass
             const double r = is_g ? g_op(x, y, getbit(bp, pos + j)) : f_ex(x, y, lmax);
             A[p * per + (1 << ls) - (1 << R) + j] = r;
         }
@@ -1009,7 +1020,7 @@ __device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane, VCache
             }
         } else if constexpr (FM == 1 && V >= 1 && PL_SCL_FEX_HOIST) {
             vvisit_ex<L, V, CPW>(t.llr, t.b0, t.bs, t.n, t.W, t.per, t.lmax, t.smem, t.y.bytes, t.y.off_A,
-                                 t.y.off_beta, s, pos, is_g ? 1 : 0, lane, t.vcache);
+                                 t.y.off_beta, s, pos, is_g ? 1 : 0, lane, t.vcache, vc, t.y.off_sptr);
         } else {
         // channel rows addressed from the wave's first row (uniform base, 32-bit lane offsets)
         const float* ch0 = t.llr + t.b0 * t.n;
@@ -1758,7 +1769,8 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
     }
 
     VCache vcache_lane;  // min-sum, n = 1024 (V = 4): the virtual node-of-64 cache (vnode64)
-    VCache* vcp = (PL_SCL_VCACHE && !PL_SCL_VPF && FM == 0 && V == 4) ? &vcache_lane : nullptr;
+    VCache* vcp = (PL_SCL_VCACHE && !PL_SCL_VPF && ((FM == 0 && V == 4) || (FM == 1 && V >= 1 && PL_SCL_FEX_HOIST)))
+                      ? &vcache_lane : nullptr;
     double pm = gl == 0 || gl == L ? 0.0 : lmax;  // :192-194 ([0, 30 x (L-1)] per half)
     const int nsub = n >> R;
     int q = 0;
