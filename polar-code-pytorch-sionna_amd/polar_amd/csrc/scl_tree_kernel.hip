@@ -530,6 +530,15 @@ __device__ __forceinline__ void vlev_path(double* vx, double* vy, const uint32_t
         vlev_path<Q - 1, FM>(vx, vy, bp, wb, j, gmask, lmax);
     }
 }
+template <int Q, int QE, int FM>  // per-path levels Q down to QE
+__device__ __forceinline__ void vlev_range(double* vx, double* vy, const uint32_t* bp, const int* wb, int j,
+                                           uint32_t gmask, double lmax) {
+    if constexpr (Q >= QE && Q >= 0) {
+        if ((gmask >> Q) & 1u) vlev_g<Q>(vx, vy, bp + wb[Q], j);
+        else vlev_f<Q, FM>(vx, vy, lmax);
+        vlev_range<Q - 1, QE, FM>(vx, vy, bp, wb, j, gmask, lmax);
+    }
+}
 template <int Q, int QE, int FM>  // shared f levels Q down to QE
 __device__ __forceinline__ void vlev_shared(double* vx, double* vy, double lmax) {
     if constexpr (Q >= QE) {
@@ -544,20 +553,32 @@ __device__ __forceinline__ void vlev_shared(double* vx, double* vy, double lmax)
 // entry is found through the owner byte sptr[p][6] (written by the left pass, re-pointed with
 // the other stage owners when paths fork), and lives in this lane's private memory: the lane that
 // handles item (c, j) in one pass handles it in every pass.  Half the passes then cost one load
-// and one g per path instead of 31 f/g.
+// and one g per path instead of 31 f/g.  Min-sum also keeps the stage-7 values (after the
+// level that produces them, in the left pass of a stage-7 node's left child): the left pass of
+// its right child then starts from them (one g per side and the f) instead of the channel.
 #ifndef PL_SCL_VCACHE
 #define PL_SCL_VCACHE 1
 #endif
+#ifndef PL_SCL_C7
+#define PL_SCL_C7 0  // 1: min-sum caches the stage-7 values too (A/B r04i: 0.942 vs 0.929 ms -- the
+                     // extra private-memory traffic costs more than the f/g it saves)
+#endif
 struct VCache {
-    double2 v[32];  // [it * L + path]: (x, y) = stage-6 elements (j, j + 32); IT * L <= 32
+    double2 v[32];   // [it * L + path]: (x, y) = stage-6 elements (j, j + 32); IT * L <= 32
+#if PL_SCL_C7
+    double4 v7[32];  // min-sum: the stage-7 elements (j, j + 64 | j + 32, j + 96) of the same path
+    int p7;          // start of the stage-7 node v7 belongs to (fast-SCL may prune the left pass
+                     // that writes it: the right child's pass then recomputes); same in every lane
+#endif
 };
 
 template <int L, int V, int NS, int FM>
 __device__ __forceinline__ void vnode64(const St& t, const Cw& w, const float* cx, const float* cy, const int* wb,
                                         int j, uint32_t gmask, bool is_g, int pos, int ls, VCache* vc = nullptr,
-                                        int it = 0) {
+                                        int it = 0, bool w7 = false) {
     constexpr int H = 1 << (V - 1);       // values per side after the channel level
-    constexpr int K = NS > 0 ? (2 * H) >> NS : 2 * H;  // per side after the shared levels
+    constexpr int NSS = (NS == V && PL_SCL_C7) ? V - 1 : NS;  // shared levels (C7: before the stage-7 boundary)
+    constexpr int K = NSS > 0 ? (2 * H) >> NSS : 2 * H;  // per side after those shared levels
     double sx[K], sy[K];
     if constexpr (NS > 0) {
         double vx[H], vy[H];
@@ -566,7 +587,7 @@ __device__ __forceinline__ void vnode64(const St& t, const Cw& w, const float* c
             vx[m] = f_op<FM>((double)cx[m], (double)cx[m + H], t.lmax);
             vy[m] = f_op<FM>((double)cy[m], (double)cy[m + H], t.lmax);
         }
-        vlev_shared<V - 2, V - NS, FM>(vx, vy, t.lmax);
+        vlev_shared<V - 2, V - NSS, FM>(vx, vy, t.lmax);
 #pragma unroll
         for (int m = 0; m < K; ++m) {
             sx[m] = vx[m];
@@ -587,14 +608,24 @@ __device__ __forceinline__ void vnode64(const St& t, const Cw& w, const float* c
                 vx[m + 1] = g_op((double)cx[m + 1], (double)cx[m + 1 + H], (u4.z >> j) & 1u);
                 vy[m + 1] = g_op((double)cy[m + 1], (double)cy[m + 1 + H], (u4.w >> j) & 1u);
             }
-            vlev_path<V - 2, FM>(vx, vy, bp, wb, j, gmask, t.lmax);
+            vlev_range<V - 2, 1, FM>(vx, vy, bp, wb, j, gmask, t.lmax);
         } else {
 #pragma unroll
             for (int m = 0; m < K; ++m) {
                 vx[m] = sx[m];
                 vy[m] = sy[m];
             }
-            vlev_path<V - NS - 1, FM>(vx, vy, bp, wb, j, gmask, t.lmax);
+            vlev_range<V - NSS - 1, 1, FM>(vx, vy, bp, wb, j, gmask, t.lmax);
+        }
+        // the stage-7 values (levels above done): cached for the right child's left pass
+#if PL_SCL_C7
+        if (w7) vc->v7[it * L + p] = make_double4(vx[0], vx[1], vy[0], vy[1]);
+#endif
+        if constexpr (NSS == V) {  // every level shared: nothing per path
+        } else if constexpr (NS == V) {  // C7: level 0 is the last shared f (same value for every path)
+            vlev_f<0, FM>(vx, vy, t.lmax);
+        } else {
+            vlev_range<0, 0, FM>(vx, vy, bp, wb, j, gmask, t.lmax);
         }
         const double x = vx[0], y = vy[0];
         if (vc != nullptr) vc->v[it * L + p] = make_double2(x, y);  // the left pass (is_g false)
@@ -614,6 +645,23 @@ __device__ __forceinline__ void vnode64_cached(const St& t, const Cw& w, int j, 
     }
 }
 
+// The left pass of a stage-7 node's right child (level 0 a g) from the stage-7 cache: per path,
+// the owner's four values, one g per side, the f, and the stage-6 entry for the right pass.
+#if PL_SCL_C7
+template <int L>
+__device__ __forceinline__ void vnode64_c7(const St& t, const Cw& w, int j, int pos, int ls, VCache& vc, int it) {
+    const int p7 = pos & ~127;  // start of the stage-7 node: the left child's partial sums
+#pragma unroll 1
+    for (int p = 0; p < L; ++p) {
+        const uint32_t* bp = w.beta + p * t.W;
+        const double4 c = vc.v7[it * L + w.sptr[p * SPS + ls + 2]];
+        const double x = g_op(c.x, c.y, getbit(bp, p7 + j)), y = g_op(c.z, c.w, getbit(bp, p7 + 32 + j));
+        vc.v[it * L + p] = make_double2(x, y);
+        w.A[p * t.per + (1 << ls) - (1 << R) + j] = f_ms(x, y, t.lmax);
+    }
+}
+#endif
+
 // One pass of a virtual node of 64 over the wave's (codeword, element) pairs; NS leading f
 // levels (a per-pass constant, so each NS is its own loop).
 template <int L, int V, int NS, int FM, int CPW>
@@ -625,6 +673,18 @@ __device__ void vvisit64(const St& t, int pos, bool is_g, int lane, const int* w
             vnode64_cached<L>(t, t.cw(idx >> ls), idx & (h - 1), pos, ls, *vc, it);
         return;
     }
+#if PL_SCL_C7
+    if (vc != nullptr && FM == 0 && (pos & 127) == 64 && vc->p7 == pos - 64) {  // right child of its stage-7 node
+#pragma unroll 1
+        for (int idx = lane, it = 0; idx < CPW * h; idx += 64, ++it)
+            vnode64_c7<L>(t, t.cw(idx >> ls), idx & (h - 1), pos, ls, *vc, it);
+        return;
+    }
+    const bool w7 = vc != nullptr && FM == 0 && (pos & 127) == 0;  // a new stage-7 node
+    if (w7) vc->p7 = pos;
+#else
+    const bool w7 = false;
+#endif
     // channel rows addressed from the wave's first row (uniform base, 32-bit lane offsets)
     const float* ch0 = t.llr + t.b0 * t.n;
 #if PL_SCL_VPF
@@ -675,7 +735,7 @@ __device__ void vvisit64(const St& t, int pos, bool is_g, int lane, const int* w
             cx[m] = -1.0f * ch0[co + m * hs];
             cy[m] = -1.0f * ch0[co + h + m * hs];
         }
-        vnode64<L, V, NS, FM>(t, w, cx, cy, wb, j, gmask, is_g, pos, ls, vc, it);
+        vnode64<L, V, NS, FM>(t, w, cx, cy, wb, j, gmask, is_g, pos, ls, vc, it, w7);
     }
 #endif
 }
@@ -1066,7 +1126,10 @@ __device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane, VCache
         uint8_t* sp = t.cw(lane >> LL).sptr + (lane & (L - 1)) * SPS;
         sp[ls] = (uint8_t)(lane & (L - 1));
         // the left pass of a cached virtual node: each path now owns its own stage-6 cache entry
-        if (vc != nullptr && !is_g && s > t.SS) sp[s] = (uint8_t)(lane & (L - 1));
+        if (vc != nullptr && !is_g && s > t.SS) {
+            sp[s] = (uint8_t)(lane & (L - 1));
+            if (PL_SCL_C7 && FM == 0 && V == 4 && (pos & 127) == 0) sp[s + 1] = (uint8_t)(lane & (L - 1));
+        }
     }
     __syncthreads();
 }
@@ -1768,7 +1831,10 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
         }
     }
 
-    VCache vcache_lane;  // min-sum, n = 1024 (V = 4): the virtual node-of-64 cache (vnode64)
+    VCache vcache_lane;  // the virtual-node cache (vnode64, vvisit_ex)
+#if PL_SCL_C7
+    vcache_lane.p7 = -1;
+#endif
     VCache* vcp = (PL_SCL_VCACHE && !PL_SCL_VPF && ((FM == 0 && V == 4) || (FM == 1 && V >= 1 && PL_SCL_FEX_HOIST)))
                       ? &vcache_lane : nullptr;
     double pm = gl == 0 || gl == L ? 0.0 : lmax;  // :192-194 ([0, 30 x (L-1)] per half)

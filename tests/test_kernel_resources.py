@@ -82,6 +82,7 @@ def test_scl_exact_f_kernels_have_no_spills():
             (m,) = meta.values()
             assert m["vgpr_spill_count"] == 0, (v, fast, m)
             # the VCache (512 B per lane, round 4) + the vterm frame (16 B, fast kernels)
+            # the VCache (512 B per lane, round 4) + the vterm frame (16 B, fast kernels)
             assert m["private_segment_fixed_size"] <= (544 if fast == "1" else 528), (v, fast, m)
             assert m["vgpr_count"] <= 256, (v, fast, m)
 
