@@ -283,12 +283,9 @@ def plan_mask(fp, n):
     return polar_amd.frozen_mask(fp, n)
 
 
-VALU_PEAK_GINSTR_S = 1024 * 2.4 / 4  # 256 CUs x 4 SIMDs, one wave64 VALU instruction per 4 cycles at 2.4 GHz
-
-
 def valu_from_profiles(tag):
-    """SQ counters per launch of this shape's kernel from the committed rocprofv3 --pmc pass
-    (profiles/valu.json, written by tools/sq_roofline.py), or None."""
+    """The VALU-issue inputs of this shape's kernel (profiles/valu.json, tools/valu_roofline.py),
+    or None."""
     path = os.path.join(ROOT, "profiles", "valu.json")
     if not os.path.exists(path):
         return None
@@ -298,21 +295,45 @@ def valu_from_profiles(tag):
         return None
 
 
-def valu_roofline(tag, kern_ms):
-    """VALU-issue roofline of the kernel: achieved = SQ_INSTS_VALU per launch (wave64 instructions,
-    counted by rocprofv3) / the launch time measured here; peak = 1024 SIMDs issuing one wave64
-    VALU instruction per 4 cycles at 2.4 GHz; busy_frac = SQ_ACTIVE_INST_VALU (quad-cycles a wave
-    spends issuing VALU work) x 4 / (1024 x 2.4 GHz x launch time)."""
-    v = valu_from_profiles(tag)
-    if not v:
+def current_isa_sha(tag):
+    """The pinned instruction-stream hash of the bench kernel (tests/golden/kernel_isa.json, which
+    tests/test_kernel_resources.py holds equal to the built kernel)."""
+    pin = {"sc_k512_n1024_bs65536": "sc_k512_n1024_minsum", "scl_k512_n1024_bs8192_L8": "scl_L8_n1024_minsum"}.get(tag)
+    try:
+        return json.load(open(os.path.join(ROOT, "tests", "golden", "kernel_isa.json")))[pin]["sha"]
+    except Exception:
         return None
-    t = kern_ms * 1e-3
-    ach = v["sq_insts_valu_per_launch"] / t / 1e9
-    out = {"bound": "valu", "achieved": round(ach, 2), "peak": VALU_PEAK_GINSTR_S, "unit": "G wave-instr/s",
-           "frac": round(ach / VALU_PEAK_GINSTR_S, 5), "kernel_ms": round(kern_ms, 5),
-           "valu_instr_per_launch": v["sq_insts_valu_per_launch"], "counter_file": v.get("source")}
-    if v.get("sq_active_inst_valu_per_launch"):
-        out["busy_frac"] = round(v["sq_active_inst_valu_per_launch"] * 4 / (1024 * 2.4e9 * t), 5)
+
+
+def valu_roofline(tag, kern_ms):
+    """VALU-issue roofline of the kernel from its measured instruction mix: per launch, the SQ
+    class counters (rocprofv3) times each class's issue cost (ns per wave-instruction per SIMD,
+    calibrated by tools/micro/valu_cycles.hip at a settled clock), summed and spread over the
+    1024 SIMDs, against the launch time measured here.  The instructions the counters leave
+    unclassified (bitwise, bitop3, moves, DPP moves, compares, selects, min/max) cost 1.0 ... 1.8
+    ns: frac_lo / frac_hi bound the fraction, frac is their mean.  No busy-cycle counter exists
+    on gfx950 (SQ_ACTIVE_INST_VALU / SQ_THREAD_CYCLES_VALU count instructions), so none is reported.
+    null fields when the profile was taken on another instruction stream than the built kernel's."""
+    v = valu_from_profiles(tag)
+    if not v or "issue_ns_simd_per_launch" not in v:
+        return None
+    out = {"bound": "valu_issue", "unit": "us of VALU issue per SIMD per launch", "kernel_ms": round(kern_ms, 5),
+           "valu_instr_per_launch": v["valu_per_launch"], "counter_files": v.get("source"),
+           "isa_sha": v.get("isa_sha")}
+    if v.get("isa_sha") != current_isa_sha(tag):
+        out.update({"stale": True, "frac": None, "frac_lo": None, "frac_hi": None})
+        return out
+    ns = v["issue_ns_simd_per_launch"]
+    simd_ns = kern_ms * 1e6 * 1024
+    lo = (ns["classified"] + ns["other_lo"]) / simd_ns
+    hi = (ns["classified"] + ns["other_hi"]) / simd_ns
+    out.update({"stale": False, "frac": round((lo + hi) / 2, 4), "frac_lo": round(lo, 4), "frac_hi": round(hi, 4),
+                # achieved = VALU issue time per SIMD and launch (mean of the bounds), peak = the launch time
+                "achieved": round((lo + hi) / 2 * kern_ms * 1e3, 2), "peak": round(kern_ms * 1e3, 2),
+                "issue_us_per_simd": [round((ns["classified"] + ns["other_lo"]) / 1024 / 1e3, 2),
+                                      round((ns["classified"] + ns["other_hi"]) / 1024 / 1e3, 2)],
+                "wait_share_per_wave": round(v["per_wave"].get("WAIT_ANY", 0) / max(v["per_wave"].get("WAVE_CYCLES", 1), 1), 4)
+                if "WAIT_ANY" in v["per_wave"] and "WAVE_CYCLES" in v["per_wave"] else None})
     return out
 
 

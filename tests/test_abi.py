@@ -251,3 +251,27 @@ def test_diagnostic_macros_refuse_release_builds(tmp_path):
                             f"-D{macro}=1", f"-I{b.OBJ}", os.path.join(b.CSRC, src)],
                            capture_output=True, text=True, timeout=300)
         assert r.returncode != 0 and "development builds" in r.stderr, (src, r.stderr[-500:])
+
+
+def test_bench_valu_roofline_from_committed_counters():
+    """bench.py's VALU-issue roofline: from profiles/valu.json (per-class SQ counters x calibrated
+    issue costs), current while the profiled instruction stream is the pinned one, reported null
+    (stale) once the kernel changes."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    for tag, ms in (("sc_k512_n1024_bs65536", 0.0814), ("scl_k512_n1024_bs8192_L8", 0.93)):
+        rv = bench.valu_roofline(tag, ms)
+        assert rv is not None and rv["stale"] is False, tag
+        assert 0.3 < rv["frac_lo"] <= rv["frac"] <= rv["frac_hi"] < 1.0
+        assert "busy_frac" not in rv
+        for f in rv["counter_files"]:
+            assert os.path.exists(os.path.join(ROOT, f)), f
+    orig = bench.current_isa_sha
+    bench.current_isa_sha = lambda tag: "0" * 16
+    try:
+        rv = bench.valu_roofline("sc_k512_n1024_bs65536", 0.0814)
+        assert rv["stale"] is True and rv["frac"] is None
+    finally:
+        bench.current_isa_sha = orig

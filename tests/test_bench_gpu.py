@@ -32,11 +32,12 @@ def test_bench_json_contract(decoder):
     rf = d["roofline"] if decoder == "sc" else d["roofline_hbm"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] == 8000.0
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-4
-    # the VALU-issue roofline from the committed SQ counters (profiles/valu.json): the list
-    # decoder's own bound; next to the HBM one for SC
+    # the VALU-issue roofline from the committed per-class SQ counters and issue costs
+    # (profiles/valu.json): the list decoder's own bound; next to the HBM one for SC
     rv = d["roofline"] if decoder == "scl" else d["roofline_valu"]
-    assert rv["bound"] == "valu" and rv["unit"] == "G wave-instr/s" and 0 < rv["frac"] < 1.2
-    assert abs(rv["frac"] - rv["achieved"] / rv["peak"]) < 1e-4 and rv["counter_file"]
+    assert rv["bound"] == "valu_issue" and rv["stale"] is False and rv["counter_files"]
+    assert 0 < rv["frac_lo"] <= rv["frac"] <= rv["frac_hi"] < 1.2
+    assert abs(rv["frac"] - rv["achieved"] / rv["peak"]) < 1e-3
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1 and cb["sample"]
     assert cb["best_of"] == 3 and cb["single_thread"]["cores"] == 1 and cb["single_thread"]["value"] > 0

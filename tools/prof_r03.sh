@@ -5,7 +5,7 @@
 #     picked out of the trace (tools/trace_window.py) next to the bench line's HIP-event figure;
 #  2. the SCL bench line and its kernel statistics;
 #  3. rocprofv3 --pmc passes, each in its own run: FETCH_SIZE, WRITE_SIZE (SC), and one SQ pass per
-#     decoder (SQ_INSTS_VALU ... GRBM_GUI_ACTIVE) for the VALU roofline (tools/sq_roofline.py).
+#     decoder (SQ_INSTS_VALU ... GRBM_GUI_ACTIVE) for the VALU roofline (tools/valu_roofline.py).
 # Every step runs under its own timeout; the first failure ends the script.
 set -eo pipefail
 TAG=${1:?usage: prof_r03.sh TAG}

@@ -5,7 +5,7 @@
 #     configs[1] / configs[3] launches and the single-wave probe (tools/trace_configs.py);
 #  2. --pmc passes, each its own run: FETCH_SIZE, WRITE_SIZE (HBM traffic of the SC kernel);
 #  3. SQ passes per decoder (VALU class counts, VALU thread-cycles, waits) for the VALU roofline
-#     (tools/sq_roofline.py), and the same counters on the calibration kernels (valu_cycles).
+#     (tools/valu_roofline.py), and the same counters on the calibration kernels (valu_cycles).
 # Every step runs under its own timeout; the first failure ends the script.
 set -eo pipefail
 TAG=${1:?usage: prof_r04.sh TAG}
