@@ -90,6 +90,26 @@ def test_specialised_kernel_compiles_without_gpu(tmp_path):
     assert buf2.value != buf.value
 
 
+def test_inprocess_hiprtc_n128_reference_codes(tmp_path):
+    """In-process hiprtc in a process that has imported torch (so torch's bundled libhiprtc /
+    amd_comgr are the ones mapped) on n = 128 reference codes, both f modes: the round-2 segfault
+    ("In-process hiprtc") does not recur -- the full sweep over the 93 codes with n <= 256,
+    with the GPU initialised, is profiles/r04l_hiprtc_inprocess_*.txt."""
+    import numpy as np
+    import torch  # noqa: F401  (load order as in a torch process)
+    from polar_amd import _lib, build as b
+    L = _lib.lib()
+    codes = [c for c in b.reference_codes() if len(c[0]) == 128]
+    codes = [c for c in codes if c[1] == 1][:1] + [c for c in codes if c[1] == 0][:2]
+    assert len(codes) == 3
+    buf = ctypes.create_string_buffer(4096)
+    for m, fm in codes:
+        m = np.ascontiguousarray(m, dtype=np.uint8)
+        rc = L.pl_sc_specialize(128, m.ctypes.data_as(ctypes.c_void_p), fm, str(tmp_path).encode(), buf, 4096)
+        assert rc == 0, L.pl_last_error_string()
+        assert b"pl_sc_static_f32" in open(buf.value.decode(), "rb").read()
+
+
 def test_reference_codes_are_prebuilt():
     """build() pre-compiles the specialised kernels of every pinned reference code."""
     from polar_amd import build as b
