@@ -88,6 +88,9 @@ namespace {
 #ifndef PL_SCL_DIAG_NO_REPOINT
 #define PL_SCL_DIAG_NO_REPOINT 0  // timing diagnostic (wrong results)
 #endif
+#ifndef PL_SCL_DIAG_NO_PULL
+#define PL_SCL_DIAG_NO_PULL 0  // timing diagnostic (wrong results)
+#endif
 #ifndef PL_SCL_DIAG_NO_COMBINE
 #define PL_SCL_DIAG_NO_COMBINE 0  // timing diagnostic (wrong results)
 #endif
@@ -105,6 +108,45 @@ namespace {
 #endif
 #ifndef PL_SCL_WPE
 #define PL_SCL_WPE 2  // > 0: amdgpu_waves_per_eu minimum (2: <= 256 VGPRs, A/B on MI355X: 2.30 vs 3.62 ms at V=4)
+#endif
+
+// Phase timing (development builds, tools/scl_prof.py): per wave, s_memtime cycles spent in each
+// phase of the decoder loop, written after the 2L-row metrics of out_pm (the caller sizes out_pm
+// for bs * 2L + waves * 12 doubles).  Phases: 0 virtual node passes (left / f), 1 stored-stage node
+// passes, 2 lane subtrees, 3 re-pointing and partial-sum stores, 4 combines, 5 pruned nodes and
+// right (g) virtual passes, 6 set-up
+// (incl. exact-f caches), 7 the final butterfly / CRC / sort / output; 8..11 split the lane subtrees
+// (min-sum, no fast-SCL): leaf f/g, penalties, ranks, selection moves (2 keeps the rest).
+#ifndef PL_SCL_PROF
+#define PL_SCL_PROF 0
+#endif
+#if PL_SCL_PROF && !PL_DEV
+#error "PL_SCL_PROF: development builds (-DPL_DEV=1) only"
+#endif
+#if PL_SCL_PROF
+constexpr int kProfSlots = 12;  // 8..11: inside the lane subtrees -- leaf f/g, penalties, ranks, selection moves
+struct Prof {
+    unsigned long long acc[kProfSlots];
+    unsigned long long t;
+};
+#define PROF_DECL                                            \
+    Prof prof;                                               \
+    _Pragma("unroll") for (int pi_ = 0; pi_ < kProfSlots; ++pi_) prof.acc[pi_] = 0; \
+    prof.t = __builtin_amdgcn_s_memtime()
+#define PROF_MARK_P(P, i)                                            \
+    do {                                                             \
+        const unsigned long long prof_n = __builtin_amdgcn_s_memtime(); \
+        (P).acc[i] += prof_n - (P).t;                                \
+        (P).t = prof_n;                                              \
+    } while (0)
+#define PROF_MARK(i) PROF_MARK_P(prof, i)
+#define PROF_PARAM , Prof& prof
+#define PROF_ARG , prof
+#else
+#define PROF_DECL
+#define PROF_MARK(i)
+#define PROF_PARAM
+#define PROF_ARG
 #endif
 
 constexpr int R = PL_SCL_R;  // stage of the lane-local subtree
@@ -560,13 +602,18 @@ __device__ __forceinline__ void vlev_shared(double* vx, double* vy, double lmax)
 #define PL_SCL_VCACHE 1
 #endif
 #ifndef PL_SCL_C7
-#define PL_SCL_C7 0  // 1: min-sum caches the stage-7 values too (A/B r04i: 0.942 vs 0.929 ms -- the
-                     // extra private-memory traffic costs more than the f/g it saves)
+#define PL_SCL_C7 1  // 1: min-sum caches the stage-7 values too (A/B r04i, one path per step: 0.942 vs
+                     // 0.929 ms; with the batched loads, r04q: 0.868 vs 0.893 ms)
 #endif
+template <int FM>
 struct VCache {
     double2 v[32];   // [it * L + path]: (x, y) = stage-6 elements (j, j + 32); IT * L <= 32
+};
+template <>
+struct VCache<0> {  // min-sum
+    double2 v[32];
 #if PL_SCL_C7
-    double4 v7[32];  // min-sum: the stage-7 elements (j, j + 64 | j + 32, j + 96) of the same path
+    double4 v7[32];  // the stage-7 elements (j, j + 64 | j + 32, j + 96) of the same path
     int p7;          // start of the stage-7 node v7 belongs to (fast-SCL may prune the left pass
                      // that writes it: the right child's pass then recomputes); same in every lane
 #endif
@@ -574,7 +621,7 @@ struct VCache {
 
 template <int L, int V, int NS, int FM>
 __device__ __forceinline__ void vnode64(const St& t, const Cw& w, const float* cx, const float* cy, const int* wb,
-                                        int j, uint32_t gmask, bool is_g, int pos, int ls, VCache* vc = nullptr,
+                                        int j, uint32_t gmask, bool is_g, int pos, int ls, VCache<FM>* vc = nullptr,
                                         int it = 0, bool w7 = false) {
     constexpr int H = 1 << (V - 1);       // values per side after the channel level
     constexpr int NSS = (NS == V && PL_SCL_C7) ? V - 1 : NS;  // shared levels (C7: before the stage-7 boundary)
@@ -633,24 +680,64 @@ __device__ __forceinline__ void vnode64(const St& t, const Cw& w, const float* c
         w.A[p * t.per + (1 << ls) - (1 << R) + j] = r;
     }
 }
-// The right pass from the cache: per path, the owner's (x, y) and one g.
-template <int L>
-__device__ __forceinline__ void vnode64_cached(const St& t, const Cw& w, int j, int pos, int ls, const VCache& vc,
+// The right pass from the cache: per path, the owner's (x, y) and one g.  Every owner byte, cache
+// entry and partial-sum word of the pass is loaded before the first g, so the private-memory loads
+// (L2 latency) overlap instead of being paid once per path (r04n phase timing: 12.7k cycles per pass
+// with one path per step).
+#ifndef PL_SCL_VC_BATCH
+#define PL_SCL_VC_BATCH 1
+#endif
+template <int L, int FM>
+__device__ __forceinline__ void vnode64_cached(const St& t, const Cw& w, int j, int pos, int ls, const VCache<FM>& vc,
                                                int it) {
+#if PL_SCL_VC_BATCH
+    int o[L];
+    uint32_t wd[L];
+#pragma unroll
+    for (int p = 0; p < L; ++p) {
+        o[p] = w.sptr[p * SPS + ls + 1];
+        wd[p] = w.beta[p * t.W + ((pos + j) >> 5)];
+    }
+    double2 xy[L];
+#pragma unroll
+    for (int p = 0; p < L; ++p) xy[p] = vc.v[it * L + o[p]];
+#pragma unroll
+    for (int p = 0; p < L; ++p)
+        w.A[p * t.per + (1 << ls) - (1 << R) + j] = g_op(xy[p].x, xy[p].y, (wd[p] >> ((pos + j) & 31)) & 1u);
+#else
 #pragma unroll 1
     for (int p = 0; p < L; ++p) {
         const int o = w.sptr[p * SPS + ls + 1];
         const double2 xy = vc.v[it * L + o];
         w.A[p * t.per + (1 << ls) - (1 << R) + j] = g_op(xy.x, xy.y, getbit(w.beta + p * t.W, pos + j));
     }
+#endif
 }
 
 // The left pass of a stage-7 node's right child (level 0 a g) from the stage-7 cache: per path,
 // the owner's four values, one g per side, the f, and the stage-6 entry for the right pass.
 #if PL_SCL_C7
 template <int L>
-__device__ __forceinline__ void vnode64_c7(const St& t, const Cw& w, int j, int pos, int ls, VCache& vc, int it) {
+__device__ __forceinline__ void vnode64_c7(const St& t, const Cw& w, int j, int pos, int ls, VCache<0>& vc, int it) {
     const int p7 = pos & ~127;  // start of the stage-7 node: the left child's partial sums
+#if PL_SCL_VC_BATCH
+    double4 c[L];
+    uint32_t wx[L], wy[L];
+#pragma unroll
+    for (int p = 0; p < L; ++p) {
+        const uint32_t* bp = w.beta + p * t.W;
+        c[p] = vc.v7[it * L + w.sptr[p * SPS + ls + 2]];
+        wx[p] = bp[(p7 + j) >> 5];
+        wy[p] = bp[(p7 + 32 + j) >> 5];
+    }
+#pragma unroll
+    for (int p = 0; p < L; ++p) {
+        const double x = g_op(c[p].x, c[p].y, (wx[p] >> ((p7 + j) & 31)) & 1u);
+        const double y = g_op(c[p].z, c[p].w, (wy[p] >> ((p7 + 32 + j) & 31)) & 1u);
+        vc.v[it * L + p] = make_double2(x, y);
+        w.A[p * t.per + (1 << ls) - (1 << R) + j] = f_ms(x, y, t.lmax);
+    }
+#else
 #pragma unroll 1
     for (int p = 0; p < L; ++p) {
         const uint32_t* bp = w.beta + p * t.W;
@@ -659,25 +746,36 @@ __device__ __forceinline__ void vnode64_c7(const St& t, const Cw& w, int j, int 
         vc.v[it * L + p] = make_double2(x, y);
         w.A[p * t.per + (1 << ls) - (1 << R) + j] = f_ms(x, y, t.lmax);
     }
+#endif
 }
 #endif
 
 // One pass of a virtual node of 64 over the wave's (codeword, element) pairs; NS leading f
 // levels (a per-pass constant, so each NS is its own loop).
 template <int L, int V, int NS, int FM, int CPW>
-__device__ void vvisit64(const St& t, int pos, bool is_g, int lane, const int* wb, uint32_t gmask, VCache* vc) {
+__device__ void vvisit64(const St& t, int pos, bool is_g, int lane, const int* wb, uint32_t gmask, VCache<FM>* vc) {
     constexpr int NC = 1 << V, ls = 5, h = 32, hs = 64;
     if (vc != nullptr && is_g) {
+#if PL_SCL_VC_BATCH
+#pragma unroll
+        for (int it = 0; it < CPW * h / 64; ++it) {
+            const int idx = lane + 64 * it;
+            vnode64_cached<L, FM>(t, t.cw(idx >> ls), idx & (h - 1), pos, ls, *vc, it);
+        }
+#else
 #pragma unroll 1
         for (int idx = lane, it = 0; idx < CPW * h; idx += 64, ++it)
-            vnode64_cached<L>(t, t.cw(idx >> ls), idx & (h - 1), pos, ls, *vc, it);
+            vnode64_cached<L, FM>(t, t.cw(idx >> ls), idx & (h - 1), pos, ls, *vc, it);
+#endif
         return;
     }
 #if PL_SCL_C7
     if (vc != nullptr && FM == 0 && (pos & 127) == 64 && vc->p7 == pos - 64) {  // right child of its stage-7 node
-#pragma unroll 1
-        for (int idx = lane, it = 0; idx < CPW * h; idx += 64, ++it)
+#pragma unroll
+        for (int it = 0; it < CPW * h / 64; ++it) {
+            const int idx = lane + 64 * it;
             vnode64_c7<L>(t, t.cw(idx >> ls), idx & (h - 1), pos, ls, *vc, it);
+        }
         return;
     }
     const bool w7 = vc != nullptr && FM == 0 && (pos & 127) == 0;  // a new stage-7 node
@@ -769,7 +867,7 @@ template <int L, int V, int CPW>
 __device__ PL_FEX_PASS_ATTR void vvisit_ex(const float* __restrict__ llr, int64_t b0, int64_t bs, int n, int W, int per,
                                        double lmax, unsigned char* smem, int cw_bytes, int off_A, int off_beta,
                                        int s, int pos, int is_g, int lane, const double* __restrict__ vcache,
-                                       VCache* vc = nullptr, int off_sptr = 0) {
+                                       VCache<1>* vc = nullptr, int off_sptr = 0) {
     // Out of line with scalar arguments only: the pass's register arrays are allocated apart from
     // the lane subtree's state (inlined, the two together spilled), and nothing goes through
     // scratch but the call's own register saves, once per pass.
@@ -805,11 +903,24 @@ __device__ PL_FEX_PASS_ATTR void vvisit_ex(const float* __restrict__ llr, int64_
         const uint32_t* beta = reinterpret_cast<const uint32_t*>(base + off_beta);
         if (vc != nullptr && is_g) {  // the right pass from the left pass's values (VCache)
             const uint8_t* sptr = base + off_sptr;
+#if PL_SCL_VC_BATCH
+            double2 xy[L];
+            uint32_t wd[L];
+#pragma unroll
+            for (int p = 0; p < L; ++p) {
+                xy[p] = vc->v[it * L + sptr[p * SPS + s]];
+                wd[p] = beta[p * W + ((pos + j) >> 5)];
+            }
+#pragma unroll
+            for (int p = 0; p < L; ++p)
+                A[p * per + (1 << ls) - (1 << R) + j] = g_op(xy[p].x, xy[p].y, (wd[p] >> ((pos + j) & 31)) & 1u);
+#else
 #pragma unroll 1
             for (int p = 0; p < L; ++p) {
                 const double2 xy = vc->v[it * L + sptr[p * SPS + s]];
                 A[p * per + (1 << ls) - (1 << R) + j] = g_op(xy.x, xy.y, getbit(beta + p * W, pos + j));
             }
+#endif
             continue;
         }
         const int co = (int)(b0 + c < bs ? c : bs - 1 - b0) * n + j;
@@ -1013,7 +1124,7 @@ __device__ __forceinline__ void node_fg_st(const St& t, int pos, bool is_g, int 
 }
 
 template <int L, int V, int FM, int CPW>
-__device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane, VCache* vc) {
+__device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane, VCache<FM>* vc) {
     constexpr int LL = ilog2(L);
     const int ls = s - 1, h = 1 << ls;
     if (PL_SCL_DIAG_SKIP_V && s > t.SS) {
@@ -1311,6 +1422,89 @@ __device__ __forceinline__ void pull_live(double* st, int i, int src) {
     }
 }
 
+// Selection by push (2L = 16): every candidate lane holds the whole state of its path (path and
+// shadow lanes mirror each other), so after ranking it sends that state -- metric, partial sums
+// with its own bit, origin and the live stage buffers -- straight to the group lane of its rank
+// with ds_permute, and each shadow lane L..2L-1 then copies its path lane (gl - L) in one DPP row
+// rotation by L restricted to the upper banks.  One LDS round trip per information leaf instead of
+// three (push the parent code, copy it to the shadows, pull the parent's state); the same values.
+// A/B r04r (min-sum, L = 8): 0.858 vs 0.864 ms.
+#ifndef PL_SCL_PUSH
+#define PL_SCL_PUSH 1
+#endif
+#ifndef PL_SCL_PUSH_DPERM
+#define PL_SCL_PUSH_DPERM 0  // 1: the shadow copies by a second ds_permute to slot (rank + L) mod 2L instead of DPP
+#endif
+template <int L>
+__device__ __forceinline__ int push_i(int v, int dst) {
+    static_assert(L == 8, "push selection: 2L = 16 (one DPP row per codeword)");
+#if PL_SCL_PUSH_DPERM
+    // dst2 = the group lane L slots away (a permutation too): slot >= L receives the candidate of
+    // rank slot - L, its path lane's
+    const int dst2 = dst ^ (L << 2);
+    const int r = __builtin_amdgcn_ds_permute(dst, v), r2 = __builtin_amdgcn_ds_permute(dst2, v);
+    return (threadIdx.x & L) ? r2 : r;
+#else
+    const int r = __builtin_amdgcn_ds_permute(dst, v);
+    return __builtin_amdgcn_update_dpp(r, r, 0x120 + L, 0xF, 0xC, false);  // row_ror:8, lanes 8..15 of each row
+#endif
+}
+template <int L>
+__device__ __forceinline__ double push_d(double v, int dst) {
+    const long long b = __double_as_longlong(v);
+    const int lo = push_i<L>((int)(b & 0xffffffffLL), dst), hi = push_i<L>((int)(b >> 32), dst);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// A live stage-s buffer whose parent stage s+1 is live too is the f of the parent's (its node is
+// the left child, and neither buffer has changed since the node began): it is recomputed from the
+// moved parent instead of moved (PL_SCL_PUSH_REFM), which halves the values moved per information
+// leaf on average (4 doubles instead of 7); the same f, so the same values (A/B r04v: 0.847 vs 0.850 ms).
+#ifndef PL_SCL_PUSH_REFM
+#define PL_SCL_PUSH_REFM 1
+#endif
+// PL_SCL_PUSH == 2: one ds_permute sends each candidate's lane index to the slot of its rank, a
+// DPP row rotation gives the shadow slots their path slot's source, and every value is then pulled
+// (ds_bpermute) from that source lane -- two round trips, one forward permute (A/B r04x: 0.848
+// vs 0.850 ms, within noise; a second forward permute for the shadows instead of the DPP copy,
+// PL_SCL_PUSH_DPERM: 0.989 ms).
+template <int L>
+__device__ __forceinline__ int pull_src(int gl_lane, int dst) {
+    const int r = __builtin_amdgcn_ds_permute(dst, gl_lane);
+    return __builtin_amdgcn_update_dpp(r, r, 0x120 + L, 0xF, 0xC, false);
+}
+template <int L, int FM, int s>
+__device__ __forceinline__ void pull2_live(double* st, int i, int src, double lmax) {
+    if constexpr (s >= 1) {
+        if (((i >> (s - 1)) & 1) == 0) {
+            if (PL_SCL_PUSH_REFM && s + 1 < R && ((i >> s) & 1) == 0) {
+                constexpr int h = 1 << s, sp = s + 1 < R ? s + 1 : s;
+#pragma unroll
+                for (int j = 0; j < h; ++j) st[IDX(s) + j] = f_op<FM>(st[IDX(sp) + j], st[IDX(sp) + j + h], lmax);
+            } else {
+#pragma unroll
+                for (int j = 0; j < (1 << s); ++j) st[IDX(s) + j] = bperm_d(st[IDX(s) + j], src);
+            }
+        }
+        pull2_live<L, FM, s - 1>(st, i, src, lmax);
+    }
+}
+template <int L, int FM, int s>
+__device__ __forceinline__ void push_live(double* st, int i, int dst, double lmax) {
+    if constexpr (s >= 1) {
+        if (((i >> (s - 1)) & 1) == 0) {
+            if (PL_SCL_PUSH_REFM && s + 1 < R && ((i >> s) & 1) == 0) {
+                constexpr int h = 1 << s, sp = s + 1 < R ? s + 1 : s;
+#pragma unroll
+                for (int j = 0; j < h; ++j) st[IDX(s) + j] = f_op<FM>(st[IDX(sp) + j], st[IDX(sp) + j + h], lmax);
+            } else {
+#pragma unroll
+                for (int j = 0; j < (1 << s); ++j) st[IDX(s) + j] = push_d<L>(st[IDX(s) + j], dst);
+            }
+        }
+        push_live<L, FM, s - 1>(st, i, dst, lmax);
+    }
+}
+
 // Selection of the L best of the 2L candidates of a codeword group: group lane c holds candidate
 // c (c < L = (state c, u=0), c >= L = (state c-L, u=1)) with metric cv.  Its rank in the stable
 // (metric, index) order comes from 2L-1 in-group broadcasts; one ds_permute then sends every
@@ -1318,10 +1512,8 @@ __device__ __forceinline__ void pull_live(double* st, int i, int src) {
 // written exactly once), and slots >= L re-shadow slot - L.  Returns the lane's new metric, the
 // path (group index) it descends from and the bit the candidate appended.
 template <int L, int FM>
-__device__ __forceinline__ void select_2l(double cv, int gl, int gbase, int lane, double& npm, int& par,
-                                          uint32_t& bit) {
+__device__ __forceinline__ int rank_2l(double cv, int gl, int lane) {
     constexpr int GW = 2 * L;
-    const bool hi = (gl & L) != 0;
     int rk = 0;
 #if PL_SCL_DIAG_NO_RANK  // timing diagnostic only (wrong selection)
     if (true) {
@@ -1339,6 +1531,13 @@ __device__ __forceinline__ void select_2l(double cv, int gl, int gbase, int lane
     } else {
         rank_rot<GW, 1>(cv, gl, lane, rk);
     }
+    return rk;
+}
+template <int L, int FM>
+__device__ __forceinline__ void select_2l(double cv, int gl, int gbase, int lane, double& npm, int& par,
+                                          uint32_t& bit) {
+    const bool hi = (gl & L) != 0;
+    const int rk = rank_2l<L, FM>(cv, gl, lane);
     const int dst = gbase + rk;
     const int code = (gl & (L - 1)) | (hi ? 256 : 0);
     const long long cb = __double_as_longlong(cv);
@@ -1416,7 +1615,7 @@ __device__ __forceinline__ double node_sum_lane(const double* v, int kind, bool 
 // and origin (path index inside the group).  FAST: fast-SCL pruning of the rate-0 / repetition
 // nodes inside the subtree (sizes 2..8; the stage-R node itself is tested by the caller).
 template <int L, int FM, int CPW, bool FAST>
-__device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, uint32_t& ps, int lane) {
+__device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, uint32_t& ps, int lane PROF_PARAM) {
     constexpr int GW = 2 * L;
     const int gl = lane & (GW - 1), gbase = lane & ~(GW - 1);
     const bool hi = (gl & L) != 0;
@@ -1443,6 +1642,7 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
         }
         if constexpr (!FAST) {
             leaf_llr<FM, L>(inA, st, ps, i, t.lmax);
+            PROF_MARK(8);
         } else {
             // the node input at stage top = R-1 (leaf 0: f of the stage-R input) or ctz(i) (g of
             // the parent's input), then the pruning descent
@@ -1519,6 +1719,40 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
             } else {
                 pm = pm + pen;
             }
+            PROF_MARK(9);
+            continue;
+        }
+#if PL_SCL_PROF
+        asm volatile("" ::"v"(pen));
+        PROF_MARK(9);
+#endif
+        if constexpr (PL_SCL_PUSH == 2 && L == 8 && FM == 0 && !PL_SCL_DIAG_NO_PULL) {
+            const double cv = pm + pen;
+            const int dst = (gbase + rank_2l<L, FM>(cv, gl, lane)) << 2;
+            const int src = pull_src<L>(lane, dst);
+            pm = bperm_d(cv, src);
+            ps = (uint32_t)bperm_i((int)(ps | ((hi ? 1u : 0u) << i)), src);
+            org = bperm_i(org, src);
+            inA = w.A + org * t.per;
+            pull2_live<L, FM, R - 1>(st, i, src, t.lmax);
+            continue;
+        }
+        if constexpr (PL_SCL_PUSH == 1 && L == 8 && FM == 0 && !PL_SCL_DIAG_NO_PULL) {  // exact f: spills (r04r)
+            const double cv = pm + pen;
+            const int dst = (gbase + rank_2l<L, FM>(cv, gl, lane)) << 2;
+#if PL_SCL_PROF
+            asm volatile("" ::"v"(dst));
+            PROF_MARK(10);
+#endif
+            pm = push_d<L>(cv, dst);
+            ps = (uint32_t)push_i<L>((int)(ps | ((hi ? 1u : 0u) << i)), dst);
+            org = push_i<L>(org, dst);
+            inA = w.A + org * t.per;
+            push_live<L, FM, R - 1>(st, i, dst, t.lmax);
+#if PL_SCL_PROF
+            asm volatile("" ::"v"(pm), "v"(ps), "v"(org));
+            PROF_MARK(11);
+#endif
             continue;
         }
         double npm;
@@ -1743,6 +1977,7 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
     const int W = t.W, LW = ilog2(W);
     const int gl = lane & (GW - 1), my_c = lane / GW;
     const Cw mine = t.cw(my_c);
+    PROF_DECL;
 
     for (int i = lane; i < CPW * L * W; i += 64) t.cw(i >> (LL + LW)).beta[i & (L * W - 1)] = 0u;
     for (int i = lane; i < CPW * L * SPS; i += 64) {
@@ -1831,11 +2066,12 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
         }
     }
 
-    VCache vcache_lane;  // the virtual-node cache (vnode64, vvisit_ex)
+    PROF_MARK(6);
+    VCache<FM> vcache_lane;  // the virtual-node cache (vnode64, vvisit_ex)
 #if PL_SCL_C7
-    vcache_lane.p7 = -1;
+    if constexpr (FM == 0) vcache_lane.p7 = -1;
 #endif
-    VCache* vcp = (PL_SCL_VCACHE && !PL_SCL_VPF && ((FM == 0 && V == 4) || (FM == 1 && V >= 1 && PL_SCL_FEX_HOIST)))
+    VCache<FM>* vcp = (PL_SCL_VCACHE && !PL_SCL_VPF && ((FM == 0 && V == 4) || (FM == 1 && V >= 1 && PL_SCL_FEX_HOIST)))
                       ? &vcache_lane : nullptr;
     double pm = gl == 0 || gl == L ? 0.0 : lmax;  // :192-194 ([0, 30 x (L-1)] per half)
     const int nsub = n >> R;
@@ -1850,8 +2086,10 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
             top = S;
         } else {
             const int tz = __builtin_ctz(i0);
-            if (!PL_SCL_DIAG_NO_UPPER && tz <= t.SS)
+            if (!PL_SCL_DIAG_NO_UPPER && tz <= t.SS) {
                 node_fg<L, V, FM, CPW>(t, tz + 1, i0 & ~((2 << tz) - 1), true, lane, vcp);
+                if (tz + 1 > t.SS) PROF_MARK(5); else PROF_MARK(1);  // 5: right (g) virtual passes
+            }
             top = tz;
         }
         int pr = 0, kind = 0;
@@ -1863,15 +2101,20 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
                     break;
                 }
             }
-            if (!PL_SCL_DIAG_NO_UPPER && s > R && s - 1 <= t.SS) node_fg<L, V, FM, CPW>(t, s, i0, false, lane, vcp);
+            if (!PL_SCL_DIAG_NO_UPPER && s > R && s - 1 <= t.SS) {
+                node_fg<L, V, FM, CPW>(t, s, i0, false, lane, vcp);
+                if (s > t.SS) PROF_MARK(0); else PROF_MARK(1);
+            }
         }
         if (FAST && kind != 0) {
             upper_prune<L, V, FM, CPW>(t, pr, i0, kind, pm, lane);
+            PROF_MARK(5);
             q += 1 << (pr - R);
         } else {
             int org;
             uint32_t ps;
-            subtree<L, FM, CPW, FAST>(t, i0, frozen_words[i0 >> 5] >> (i0 & 31), pm, org, ps, lane);
+            subtree<L, FM, CPW, FAST>(t, i0, frozen_words[i0 >> 5] >> (i0 & 31), pm, org, ps, lane PROF_ARG);
+            PROF_MARK(2);
             // re-point the upper-tree state of every path to its origin's, then store the
             // subtree's partial sums: partial-sum words before i0 and stage owners R..SS
             if (gl < L) mine.org_s[gl] = org;
@@ -1883,6 +2126,7 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
                 *bw = off == 0 ? ps : ((*bw & ((1u << off) - 1u)) | (ps << off));
             }
             __syncthreads();
+            PROF_MARK(3);
             q += 1;
         }
         // nodes above R that end here
@@ -1890,6 +2134,7 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
         const int top2 = nxt < n ? __builtin_ctz(nxt) : S;
         if (!PL_SCL_DIAG_NO_COMBINE)
             for (int s = R + 1; s <= top2; ++s) combine_upper<L, CPW>(t, s, nxt - (1 << s), lane);
+        PROF_MARK(4);
     }
     if (gl < L) mine.pm_s[gl] = pm;
 
@@ -1973,6 +2218,15 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
             else static_cast<uint8_t*>(out)[b * k + m] = (uint8_t)bit;
         }
     }
+#if PL_SCL_PROF
+    PROF_MARK(7);
+    if (out_pm != nullptr && lane < kProfSlots) {
+        unsigned long long v = prof.acc[0];
+#pragma unroll
+        for (int i = 1; i < kProfSlots; ++i) v = lane == i ? prof.acc[i] : v;
+        reinterpret_cast<unsigned long long*>(out_pm)[bs * GW + (int64_t)blockIdx.x * kProfSlots + lane] = v;
+    }
+#endif
 }
 
 }  // namespace

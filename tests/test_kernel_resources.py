@@ -64,9 +64,10 @@ def test_scl_bench_kernel_has_no_spills_or_scratch():
     assert len(meta) == 1, list(meta)
     (m,) = meta.values()
     assert m["vgpr_spill_count"] == 0, m
-    # private memory: only the per-lane virtual node-of-64 cache (VCache, 512 B; round 4, A/B
-    # 0.925 vs 0.978 ms) and the 16-byte frame -- no register spills
-    assert m["private_segment_fixed_size"] <= 528, m
+    # private memory: only the per-lane virtual node-of-64 cache (VCache: the stage-6 entries, 512 B,
+    # A/B r04g 0.925 vs 0.978 ms; the stage-7 entries, 1 KB, A/B r04q 0.868 vs 0.893 ms) and the
+    # 16-byte frame -- no register spills
+    assert m["private_segment_fixed_size"] <= 1616, m
     assert m["vgpr_count"] <= 256, m  # amdgpu_waves_per_eu(2)
 
 
@@ -81,7 +82,6 @@ def test_scl_exact_f_kernels_have_no_spills():
             assert len(meta) == 1, (v, fast, list(meta))
             (m,) = meta.values()
             assert m["vgpr_spill_count"] == 0, (v, fast, m)
-            # the VCache (512 B per lane, round 4) + the vterm frame (16 B, fast kernels)
             # the VCache (512 B per lane, round 4) + the vterm frame (16 B, fast kernels)
             assert m["private_segment_fixed_size"] <= (544 if fast == "1" else 528), (v, fast, m)
             assert m["vgpr_count"] <= 256, (v, fast, m)
