@@ -207,6 +207,8 @@ int pl_sc_sim_count(const pl_plan* plan, uint64_t seed, uint64_t iteration, int6
                     void* hip_stream);
 
 const char* pl_last_error_string(void);
+/* "polar_mi355x <version> (gfx950) src <16 hex digits>": the FNV-1a hash of the sources the library was
+ * built from (polar_amd/build.py source_hash()). */
 const char* pl_version(void);
 
 #ifdef __cplusplus
