@@ -605,6 +605,9 @@ __device__ __forceinline__ void vlev_shared(double* vx, double* vy, double lmax)
 #define PL_SCL_C7 1  // 1: min-sum caches the stage-7 values too (A/B r04i, one path per step: 0.942 vs
                      // 0.929 ms; with the batched loads, r04q: 0.868 vs 0.893 ms)
 #endif
+// The stage-7 cache at L <= 8 only: the wider lists' kernels spill with it (L = 16: 38 VGPRs).
+template <int L, int FM>
+constexpr bool c7_on() { return PL_SCL_C7 && FM == 0 && L <= 8; }
 template <int FM>
 struct VCache {
     double2 v[32];   // [it * L + path]: (x, y) = stage-6 elements (j, j + 32); IT * L <= 32
@@ -624,7 +627,7 @@ __device__ __forceinline__ void vnode64(const St& t, const Cw& w, const float* c
                                         int j, uint32_t gmask, bool is_g, int pos, int ls, VCache<FM>* vc = nullptr,
                                         int it = 0, bool w7 = false) {
     constexpr int H = 1 << (V - 1);       // values per side after the channel level
-    constexpr int NSS = (NS == V && PL_SCL_C7) ? V - 1 : NS;  // shared levels (C7: before the stage-7 boundary)
+    constexpr int NSS = (NS == V && c7_on<L, FM>()) ? V - 1 : NS;  // shared levels (C7: before the stage-7 boundary)
     constexpr int K = NSS > 0 ? (2 * H) >> NSS : 2 * H;  // per side after those shared levels
     double sx[K], sy[K];
     if constexpr (NS > 0) {
@@ -691,19 +694,23 @@ template <int L, int FM>
 __device__ __forceinline__ void vnode64_cached(const St& t, const Cw& w, int j, int pos, int ls, const VCache<FM>& vc,
                                                int it) {
 #if PL_SCL_VC_BATCH
-    int o[L];
-    uint32_t wd[L];
+    constexpr int B = L < 8 ? L : 8;  // paths per batch (registers: 6 per path)
 #pragma unroll
-    for (int p = 0; p < L; ++p) {
-        o[p] = w.sptr[p * SPS + ls + 1];
-        wd[p] = w.beta[p * t.W + ((pos + j) >> 5)];
+    for (int p0 = 0; p0 < L; p0 += B) {
+        int o[B];
+        uint32_t wd[B];
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+            o[q] = w.sptr[(p0 + q) * SPS + ls + 1];
+            wd[q] = w.beta[(p0 + q) * t.W + ((pos + j) >> 5)];
+        }
+        double2 xy[B];
+#pragma unroll
+        for (int q = 0; q < B; ++q) xy[q] = vc.v[it * L + o[q]];
+#pragma unroll
+        for (int q = 0; q < B; ++q)
+            w.A[(p0 + q) * t.per + (1 << ls) - (1 << R) + j] = g_op(xy[q].x, xy[q].y, (wd[q] >> ((pos + j) & 31)) & 1u);
     }
-    double2 xy[L];
-#pragma unroll
-    for (int p = 0; p < L; ++p) xy[p] = vc.v[it * L + o[p]];
-#pragma unroll
-    for (int p = 0; p < L; ++p)
-        w.A[p * t.per + (1 << ls) - (1 << R) + j] = g_op(xy[p].x, xy[p].y, (wd[p] >> ((pos + j) & 31)) & 1u);
 #else
 #pragma unroll 1
     for (int p = 0; p < L; ++p) {
@@ -721,21 +728,25 @@ template <int L>
 __device__ __forceinline__ void vnode64_c7(const St& t, const Cw& w, int j, int pos, int ls, VCache<0>& vc, int it) {
     const int p7 = pos & ~127;  // start of the stage-7 node: the left child's partial sums
 #if PL_SCL_VC_BATCH
-    double4 c[L];
-    uint32_t wx[L], wy[L];
+    constexpr int B = L < 8 ? L : 8;  // paths per batch (registers: 10 per path)
 #pragma unroll
-    for (int p = 0; p < L; ++p) {
-        const uint32_t* bp = w.beta + p * t.W;
-        c[p] = vc.v7[it * L + w.sptr[p * SPS + ls + 2]];
-        wx[p] = bp[(p7 + j) >> 5];
-        wy[p] = bp[(p7 + 32 + j) >> 5];
-    }
+    for (int p0 = 0; p0 < L; p0 += B) {
+        double4 c[B];
+        uint32_t wx[B], wy[B];
 #pragma unroll
-    for (int p = 0; p < L; ++p) {
-        const double x = g_op(c[p].x, c[p].y, (wx[p] >> ((p7 + j) & 31)) & 1u);
-        const double y = g_op(c[p].z, c[p].w, (wy[p] >> ((p7 + 32 + j) & 31)) & 1u);
-        vc.v[it * L + p] = make_double2(x, y);
-        w.A[p * t.per + (1 << ls) - (1 << R) + j] = f_ms(x, y, t.lmax);
+        for (int q = 0; q < B; ++q) {
+            const uint32_t* bp = w.beta + (p0 + q) * t.W;
+            c[q] = vc.v7[it * L + w.sptr[(p0 + q) * SPS + ls + 2]];
+            wx[q] = bp[(p7 + j) >> 5];
+            wy[q] = bp[(p7 + 32 + j) >> 5];
+        }
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+            const double x = g_op(c[q].x, c[q].y, (wx[q] >> ((p7 + j) & 31)) & 1u);
+            const double y = g_op(c[q].z, c[q].w, (wy[q] >> ((p7 + 32 + j) & 31)) & 1u);
+            vc.v[it * L + p0 + q] = make_double2(x, y);
+            w.A[(p0 + q) * t.per + (1 << ls) - (1 << R) + j] = f_ms(x, y, t.lmax);
+        }
     }
 #else
 #pragma unroll 1
@@ -758,9 +769,9 @@ __device__ void vvisit64(const St& t, int pos, bool is_g, int lane, const int* w
     if (vc != nullptr && is_g) {
 #if PL_SCL_VC_BATCH
 #pragma unroll
-        for (int it = 0; it < CPW * h / 64; ++it) {
+        for (int it = 0; it < (CPW * h + 63) / 64; ++it) {  // CPW * h = 32 at L = 32: half the lanes
             const int idx = lane + 64 * it;
-            vnode64_cached<L, FM>(t, t.cw(idx >> ls), idx & (h - 1), pos, ls, *vc, it);
+            if (CPW * h % 64 == 0 || idx < CPW * h) vnode64_cached<L, FM>(t, t.cw(idx >> ls), idx & (h - 1), pos, ls, *vc, it);
         }
 #else
 #pragma unroll 1
@@ -770,15 +781,15 @@ __device__ void vvisit64(const St& t, int pos, bool is_g, int lane, const int* w
         return;
     }
 #if PL_SCL_C7
-    if (vc != nullptr && FM == 0 && (pos & 127) == 64 && vc->p7 == pos - 64) {  // right child of its stage-7 node
+    if (c7_on<L, FM>() && vc != nullptr && (pos & 127) == 64 && vc->p7 == pos - 64) {  // right child of its stage-7 node
 #pragma unroll
-        for (int it = 0; it < CPW * h / 64; ++it) {
+        for (int it = 0; it < (CPW * h + 63) / 64; ++it) {
             const int idx = lane + 64 * it;
-            vnode64_c7<L>(t, t.cw(idx >> ls), idx & (h - 1), pos, ls, *vc, it);
+            if (CPW * h % 64 == 0 || idx < CPW * h) vnode64_c7<L>(t, t.cw(idx >> ls), idx & (h - 1), pos, ls, *vc, it);
         }
         return;
     }
-    const bool w7 = vc != nullptr && FM == 0 && (pos & 127) == 0;  // a new stage-7 node
+    const bool w7 = c7_on<L, FM>() && vc != nullptr && (pos & 127) == 0;  // a new stage-7 node
     if (w7) vc->p7 = pos;
 #else
     const bool w7 = false;
@@ -904,16 +915,21 @@ __device__ PL_FEX_PASS_ATTR void vvisit_ex(const float* __restrict__ llr, int64_
         if (vc != nullptr && is_g) {  // the right pass from the left pass's values (VCache)
             const uint8_t* sptr = base + off_sptr;
 #if PL_SCL_VC_BATCH
-            double2 xy[L];
-            uint32_t wd[L];
+            constexpr int B = L <= 8 ? L : 1;  // paths per batch (wider lists: one, as before)
 #pragma unroll
-            for (int p = 0; p < L; ++p) {
-                xy[p] = vc->v[it * L + sptr[p * SPS + s]];
-                wd[p] = beta[p * W + ((pos + j) >> 5)];
+            for (int p0 = 0; p0 < L; p0 += B) {
+                double2 xy[B];
+                uint32_t wd[B];
+#pragma unroll
+                for (int q = 0; q < B; ++q) {
+                    xy[q] = vc->v[it * L + sptr[(p0 + q) * SPS + s]];
+                    wd[q] = beta[(p0 + q) * W + ((pos + j) >> 5)];
+                }
+#pragma unroll
+                for (int q = 0; q < B; ++q)
+                    A[(p0 + q) * per + (1 << ls) - (1 << R) + j] =
+                        g_op(xy[q].x, xy[q].y, (wd[q] >> ((pos + j) & 31)) & 1u);
             }
-#pragma unroll
-            for (int p = 0; p < L; ++p)
-                A[p * per + (1 << ls) - (1 << R) + j] = g_op(xy[p].x, xy[p].y, (wd[p] >> ((pos + j) & 31)) & 1u);
 #else
 #pragma unroll 1
             for (int p = 0; p < L; ++p) {
@@ -1239,7 +1255,7 @@ __device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane, VCache
         // the left pass of a cached virtual node: each path now owns its own stage-6 cache entry
         if (vc != nullptr && !is_g && s > t.SS) {
             sp[s] = (uint8_t)(lane & (L - 1));
-            if (PL_SCL_C7 && FM == 0 && V == 4 && (pos & 127) == 0) sp[s + 1] = (uint8_t)(lane & (L - 1));
+            if (c7_on<L, FM>() && V == 4 && (pos & 127) == 0) sp[s + 1] = (uint8_t)(lane & (L - 1));
         }
     }
     __syncthreads();

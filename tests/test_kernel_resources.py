@@ -87,6 +87,19 @@ def test_scl_exact_f_kernels_have_no_spills():
             assert m["vgpr_count"] <= 256, (v, fast, m)
 
 
+@pytest.mark.parametrize("L", [16, 32])
+def test_scl_wide_list_minsum_kernels_have_no_spills(L):
+    """The min-sum subtree kernels of the wider lists (one or two codewords per wave): no VGPR
+    spills (the round-4 stage-7 cache spilled 38 VGPRs at L = 16 and is on at L <= 8 only)."""
+    src = os.path.join(_build.CSRC, "scl_tree_kernel.hip")
+    with tempfile.TemporaryDirectory() as td:
+        asm = _compile_asm(src, [f"-DPL_SCL_TREE_L={L}"], td)
+    meta = _kernel_meta(asm, lambda n: f"scl_tree_kernelILi{L}E" in n and "ELi0ELb" in n)
+    assert len(meta) == 10, list(meta)  # V = 0..4, fast-SCL off / on
+    for name, m in meta.items():
+        assert m["vgpr_spill_count"] == 0, (name, m)
+
+
 def test_sc_bench_kernel_fits_four_waves_per_simd():
     import polar_amd
     from polar_amd import _lib
