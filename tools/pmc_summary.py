@@ -1,7 +1,7 @@
 """Summarise one round's rocprofv3 --pmc passes (tools/prof_round.sh TAG) into
 profiles/TAG_pmc_summary.csv and refresh profiles/traffic.json (the `traffic` bench.py reports).
 
-  python tools/pmc_summary.py TAG        (reads gpurun_out/TAG_pmc_{sc,scl}_{FETCH,WRITE}_SIZE.csv)
+  python tools/pmc_summary.py TAG [sc|scl ...]   (reads gpurun_out/TAG_pmc_{sc,scl}_{FETCH,WRITE}_SIZE.csv)
 
 FETCH_SIZE is doubled for the HBM byte count, per MI355X_MICROARCH.md (gfx950 reports half of a
 coalesced streaming read); counters are KB (x1024).
@@ -32,7 +32,9 @@ def main(tag):
     rows = [("bench", "kernel", "counter", "dispatches", "mean_kb_per_dispatch")]
     tj_path = os.path.join(ROOT, "profiles", "traffic.json")
     tj = json.load(open(tj_path))
-    for dec, kname in KERNELS.items():
+    decs = sys.argv[2:] or list(KERNELS)  # a round may profile one decoder only
+    for dec in decs:
+        kname = KERNELS[dec]
         kb = {}
         for c in ("FETCH_SIZE", "WRITE_SIZE"):
             n, m = mean_kb(os.path.join(out, f"{tag}_pmc_{dec}_{c}.csv"), kname)
@@ -44,6 +46,7 @@ def main(tag):
         e["hbm_bytes_per_launch"] = int(round((2 * kb["FETCH_SIZE"] + kb["WRITE_SIZE"]) * 1024))
         e["note"] = re.sub(r"profiles/r01\w_pmc_summary\.csv", f"profiles/{tag}_pmc_summary.csv", e["note"])
         e["note"] = re.sub(r"tools/prof_round\.sh r01\w", f"tools/prof_round.sh {tag}", e["note"])
+        e["source"] = [f"profiles/{tag}_pmc_summary.csv"]
     with open(os.path.join(ROOT, "profiles", f"{tag}_pmc_summary.csv"), "w", newline="") as f:
         csv.writer(f).writerows(rows)
     with open(tj_path, "w") as f:
