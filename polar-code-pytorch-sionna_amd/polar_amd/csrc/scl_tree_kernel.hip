@@ -114,9 +114,9 @@ namespace {
 // phase of the decoder loop, written after the 2L-row metrics of out_pm (the caller sizes out_pm
 // for bs * 2L + waves * 12 doubles).  Phases: 0 virtual node passes (left / f), 1 stored-stage node
 // passes, 2 lane subtrees, 3 re-pointing and partial-sum stores, 4 combines, 5 pruned nodes and
-// right (g) virtual passes, 6 set-up
-// (incl. exact-f caches), 7 the final butterfly / CRC / sort / output; 8..11 split the lane subtrees
-// (min-sum, no fast-SCL): leaf f/g, penalties, ranks, selection moves (2 keeps the rest).
+// right (g) virtual passes, 6 set-up (incl. exact-f caches), 7 the final butterfly / CRC / sort /
+// output; 8..11 split the lane subtrees (min-sum, no fast-SCL): leaf f/g, penalties, ranks,
+// selection moves (2 keeps the rest).
 #ifndef PL_SCL_PROF
 #define PL_SCL_PROF 0
 #endif
