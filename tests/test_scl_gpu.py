@@ -174,6 +174,24 @@ def test_scl_bench_shape_sample(pa):
     assert torch.equal(clean, u)
 
 
+@pytest.mark.parametrize("log_n", [8, 10])
+def test_scl_l8_quantized_ties(pa, log_n):
+    """L = 8, min-sum, the bench kernel's round-4 paths (selection by push, the virtual-node and
+    stage-7 caches) on LLRs drawn from {-2, -1, 0, 1, 2}: many candidates with exactly equal
+    metrics, so every stable (metric, index) tie-break is exercised.  Bits and metrics identical
+    to the generic kernel's; bits identical to the oracle's on a sample."""
+    n = 1 << log_n
+    fp = pa.reference_frozen_pos(n // 2, n).numpy()
+    rng = np.random.default_rng(77 + log_n)
+    llr = rng.integers(-2, 3, size=(257, n)).astype(np.float32)
+    x = torch.from_numpy(llr).cuda()
+    b1, pm1 = pa.ops.scl_decode(_plan(pa, fp, n, 8, "subtree"), x, return_pm=True)
+    b2, pm2 = pa.ops.scl_decode(_plan(pa, fp, n, 8, "generic"), x, return_pm=True)
+    assert torch.equal(b1, b2) and torch.equal(pm1, pm2)
+    want, _ = oracle.scl_decode(llr[:16], fp, 8, lazy=True)
+    assert np.array_equal(b1[:16].cpu().numpy(), want)
+
+
 def test_scl_edge_cases(pa):
     fp = pa.reference_frozen_pos(32, 64).numpy()
     plan = _plan(pa, fp, 64, 8)
