@@ -367,6 +367,7 @@ __global__ __launch_bounds__(64) void scl_decode_kernel(const float* __restrict_
     const Lay y = make_layout(n, log_n, L);
     const int lane = threadIdx.x;
     const int64_t b = blockIdx.x;
+    pl::sp_load_tables(lane, 64);  // the penalty's log table (softplus.h, PL_SP_FORM 3)
     St t;
     t.A = reinterpret_cast<double*>(smem + y.off_alpha);
     t.ch = reinterpret_cast<float*>(smem + y.off_ch);

@@ -1993,6 +1993,7 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
     const int W = t.W, LW = ilog2(W);
     const int gl = lane & (GW - 1), my_c = lane / GW;
     const Cw mine = t.cw(my_c);
+    pl::sp_load_tables(lane, 64);  // the penalty's log table (softplus.h, PL_SP_FORM 3)
     PROF_DECL;
 
     for (int i = lane; i < CPW * L * W; i += 64) t.cw(i >> (LL + LW)).beta[i & (L * W - 1)] = 0u;

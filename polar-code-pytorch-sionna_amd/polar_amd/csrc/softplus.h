@@ -212,8 +212,194 @@ __device__ __forceinline__ double pm_log_e(double y) {  // y >= 1, finite
     const double de = (double)e;
     return fma(de, kLn2Hi, fma(de, kLn2Lo, lm));
 }
+// PL_SP_FORM 3: the log table-driven (no division).  y = 1 + e^z >= 1, so y = 2^e m with
+// m in [1, 2): cell j = the top 7 bits of m's fraction, r = m c_j - 1 (one fma; |r| <= 2^-8, 2^-7 in
+// cell 0 where c_0 = 1), ln y = e ln2 + (-ln c_j) + log1p(r) with log1p by degree 8 (remainder
+// < 2^-59 relative) -- 21 VALU and one 16-byte LDS read instead of ~30 VALU with a reciprocal and
+// two Newton steps.  The table (2 KB) lives in LDS: kernels that evaluate the penalty call
+// sp_load_tables() at entry (all threads of the work-group, then a barrier).  Not the default:
+// A/B r04zd, SCL (512,1024) L = 8, bs = 8192: min-sum 0.857 vs 0.850 ms (the LDS read sits on the
+// leaf's dependent chain), my_sn exact + fast-SCL 1.915 vs 1.961 ms but with 7 VGPRs spilled.
+struct SpCell {
+    float c;    // c_j
+    float lo;   // -ln c_j - hi
+    double hi;  // -ln c_j rounded to fp64
+};
+// ---- BEGIN GENERATED SP TABLE (tools/gen_sp_tables.py) ----
+// {c_j (fp32), lo(-ln c_j) (fp32), hi(-ln c_j) (fp64)} per cell j of m in [1, 2)
+__device__ const SpCell kSpLogTab[128] = {
+    {0x1.0000000000000p+0f, 0.0f, 0x0.0p+0},
+    {0x1.fa11ca0000000p-1f, 0x1.8494a20000000p-61f, 0x1.7dc49e7810addp-7},
+    {0x1.f6310a0000000p-1f, -0x1.765a220000000p-61f, 0x1.3cea5df46a5c8p-6},
+    {0x1.f25f640000000p-1f, 0x1.ea33420000000p-65f, 0x1.b9fc0afaf91a1p-6},
+    {0x1.ee9c800000000p-1f, -0x1.e9ae9e0000000p-60f, 0x1.1b0d90923d990p-5},
+    {0x1.eae8080000000p-1f, 0x1.c6a8e80000000p-61f, 0x1.58a5b57c8e4dcp-5},
+    {0x1.e741aa0000000p-1f, 0x1.e683b00000000p-61f, 0x1.95c836cc8e3f4p-5},
+    {0x1.e3a9180000000p-1f, -0x1.7870f00000000p-59f, 0x1.d276b22db0b5dp-5},
+    {0x1.e01e020000000p-1f, -0x1.fb25ac0000000p-59f, 0x1.075982498e472p-4},
+    {0x1.dca01e0000000p-1f, -0x1.8a125a0000000p-58f, 0x1.253f6120a1419p-4},
+    {0x1.d92f220000000p-1f, -0x1.5f15820000000p-58f, 0x1.42edcd9a646f2p-4},
+    {0x1.d5cac80000000p-1f, -0x1.1884580000000p-58f, 0x1.60658ad3750c4p-4},
+    {0x1.d272ca0000000p-1f, -0x1.73b7f00000000p-60f, 0x1.7da76907b12cfp-4},
+    {0x1.cf26e60000000p-1f, -0x1.c99e340000000p-63f, 0x1.9ab42252033afp-4},
+    {0x1.cbe6da0000000p-1f, -0x1.fcf0f40000000p-58f, 0x1.b78c7d2b0edb1p-4},
+    {0x1.c8b2660000000p-1f, 0x1.4b0dd80000000p-58f, 0x1.d4313a96cb361p-4},
+    {0x1.c5894e0000000p-1f, -0x1.80d0c40000000p-62f, 0x1.f0a30391162cap-4},
+    {0x1.c26b540000000p-1f, -0x1.4e737a0000000p-59f, 0x1.06714f3ca5972p-3},
+    {0x1.bf583e0000000p-1f, -0x1.4477d40000000p-57f, 0x1.14785c6e742bep-3},
+    {0x1.bc4fd60000000p-1f, 0x1.e47c080000000p-61f, 0x1.2266f328a5acep-3},
+    {0x1.b951e20000000p-1f, 0x1.6b519a0000000p-57f, 0x1.303d74c647fddp-3},
+    {0x1.b65e2e0000000p-1f, -0x1.93a8da0000000p-62f, 0x1.3dfc2c26cc62bp-3},
+    {0x1.b374840000000p-1f, -0x1.f367da0000000p-57f, 0x1.4ba37269a55f0p-3},
+    {0x1.b094b40000000p-1f, 0x1.7116d20000000p-57f, 0x1.5933896982097p-3},
+    {0x1.adbe880000000p-1f, -0x1.d201ca0000000p-59f, 0x1.66acd4072ad51p-3},
+    {0x1.aaf1d20000000p-1f, 0x1.dfce1e0000000p-57f, 0x1.740f93fc037bap-3},
+    {0x1.a82e660000000p-1f, -0x1.89e4bc0000000p-58f, 0x1.815c059c357ffp-3},
+    {0x1.a574100000000p-1f, -0x1.169d820000000p-57f, 0x1.8e92902886d46p-3},
+    {0x1.a2c2a80000000p-1f, -0x1.8a1c9a0000000p-61f, 0x1.9bb36547dfb89p-3},
+    {0x1.a01a020000000p-1f, 0x1.493c820000000p-58f, 0x1.a8becdf082f1cp-3},
+    {0x1.9d79f20000000p-1f, 0x1.f327f80000000p-57f, 0x1.b5b51740fb5abp-3},
+    {0x1.9ae24e0000000p-1f, -0x1.6f6c360000000p-64f, 0x1.c2968890c18cbp-3},
+    {0x1.9852f00000000p-1f, 0x1.639a220000000p-57f, 0x1.cf6359209c5eep-3},
+    {0x1.95cbb00000000p-1f, 0x1.c34c640000000p-57f, 0x1.dc1bcdcabec8bp-3},
+    {0x1.934c680000000p-1f, -0x1.2e03a40000000p-59f, 0x1.e8c0250aa5a60p-3},
+    {0x1.90d4f20000000p-1f, -0x1.5057e20000000p-64f, 0x1.f550a0ecb7b4bp-3},
+    {0x1.8e65280000000p-1f, 0x1.88d52c0000000p-58f, 0x1.00e6c38ad501ep-2},
+    {0x1.8bfce80000000p-1f, 0x1.f170800000000p-58f, 0x1.071b860cd590dp-2},
+    {0x1.899c100000000p-1f, 0x1.a1f63c0000000p-56f, 0x1.0d46b3d9ab750p-2},
+    {0x1.87427c0000000p-1f, -0x1.0a675a0000000p-58f, 0x1.13686fa13a8b1p-2},
+    {0x1.84f00c0000000p-1f, -0x1.10c2e40000000p-56f, 0x1.1980d34542370p-2},
+    {0x1.82a4a00000000p-1f, -0x1.49fdfa0000000p-56f, 0x1.1f8ffa248a2f3p-2},
+    {0x1.8060180000000p-1f, -0x1.deed8a0000000p-59f, 0x1.2596011df763ap-2},
+    {0x1.7e22560000000p-1f, -0x1.64eb740000000p-56f, 0x1.2b93013789d31p-2},
+    {0x1.7beb3a0000000p-1f, -0x1.7135ba0000000p-57f, 0x1.31871a4144190p-2},
+    {0x1.79baa60000000p-1f, -0x1.6c58920000000p-57f, 0x1.37726827fd863p-2},
+    {0x1.7790820000000p-1f, -0x1.bea6700000000p-56f, 0x1.3d54f7e81f71cp-2},
+    {0x1.756cac0000000p-1f, -0x1.bc98b80000000p-59f, 0x1.432ef2f84e814p-2},
+    {0x1.734f0c0000000p-1f, 0x1.c201e60000000p-56f, 0x1.490068ec009d2p-2},
+    {0x1.7137860000000p-1f, -0x1.7450d80000000p-57f, 0x1.4ec9758200275p-2},
+    {0x1.6f26020000000p-1f, -0x1.a89d020000000p-57f, 0x1.548a2aa6dd268p-2},
+    {0x1.6d1a620000000p-1f, 0x1.b386940000000p-57f, 0x1.5a42ac334cfe4p-2},
+    {0x1.6b14900000000p-1f, -0x1.7c60de0000000p-57f, 0x1.5ff308ea793dbp-2},
+    {0x1.6914740000000p-1f, 0x1.896c2a0000000p-56f, 0x1.659b56383e1f4p-2},
+    {0x1.6719f40000000p-1f, -0x1.e215d20000000p-58f, 0x1.6b3bb05b59444p-2},
+    {0x1.6524f80000000p-1f, -0x1.a166400000000p-56f, 0x1.70d42f1789238p-2},
+    {0x1.63356c0000000p-1f, 0x1.7695120000000p-56f, 0x1.7664dfcb9dbd2p-2},
+    {0x1.614b360000000p-1f, 0x1.8fc38c0000000p-60f, 0x1.7bede21f7afc4p-2},
+    {0x1.5f66440000000p-1f, 0x1.1b85140000000p-61f, 0x1.816f3fb20d49fp-2},
+    {0x1.5d867c0000000p-1f, 0x1.27cd8e0000000p-58f, 0x1.86e91a5b30ba1p-2},
+    {0x1.5babcc0000000p-1f, 0x1.a2a9640000000p-57f, 0x1.8c5b7dad8b48dp-2},
+    {0x1.59d6200000000p-1f, -0x1.60e0ca0000000p-56f, 0x1.91c67bf45a84dp-2},
+    {0x1.5805600000000p-1f, -0x1.da3f620000000p-56f, 0x1.972a345135159p-2},
+    {0x1.56397c0000000p-1f, -0x1.0f7eec0000000p-56f, 0x1.9c86af25c0865p-2},
+    {0x1.54725e0000000p-1f, -0x1.9f6d760000000p-56f, 0x1.a1dc07915b999p-2},
+    {0x1.52aff60000000p-1f, 0x1.4b1da60000000p-56f, 0x1.a72a47a2bd9f0p-2},
+    {0x1.50f22e0000000p-1f, 0x1.0958f60000000p-57f, 0x1.ac718c598b0e4p-2},
+    {0x1.4f38f60000000p-1f, 0x1.18f2c80000000p-61f, 0x1.b1b1e177dfc5cp-2},
+    {0x1.4d843c0000000p-1f, -0x1.28dbcc0000000p-56f, 0x1.b6eb599bcf35ep-2},
+    {0x1.4bd3ee0000000p-1f, -0x1.5197900000000p-56f, 0x1.bc1e083cdad0bp-2},
+    {0x1.4a27fa0000000p-1f, 0x1.2bc35e0000000p-56f, 0x1.c14a01ad5f034p-2},
+    {0x1.4880520000000p-1f, 0x1.afb5c60000000p-57f, 0x1.c66f4ea3f6ff8p-2},
+    {0x1.46dce40000000p-1f, 0x1.97bbb40000000p-56f, 0x1.cb8e04fcd7ad4p-2},
+    {0x1.453d9e0000000p-1f, -0x1.0619900000000p-56f, 0x1.d0a63b7321e65p-2},
+    {0x1.43a2740000000p-1f, 0x1.5c41360000000p-57f, 0x1.d5b7f6a62c696p-2},
+    {0x1.420b520000000p-1f, 0x1.5cb9a80000000p-56f, 0x1.dac35526c5957p-2},
+    {0x1.40782e0000000p-1f, 0x1.0984580000000p-58f, 0x1.dfc856946d5c7p-2},
+    {0x1.3ee8f40000000p-1f, -0x1.0ac36e0000000p-56f, 0x1.e4c71b0e87705p-2},
+    {0x1.3d5d9a0000000p-1f, 0x1.a8eb720000000p-58f, 0x1.e9bfa37586206p-2},
+    {0x1.3bd60e0000000p-1f, 0x1.3a6e2c0000000p-58f, 0x1.eeb20b000ddf8p-2},
+    {0x1.3a52440000000p-1f, 0x1.f601c00000000p-56f, 0x1.f39e5a4011e60p-2},
+    {0x1.38d22e0000000p-1f, 0x1.de0ace0000000p-56f, 0x1.f884a0dbe9ecfp-2},
+    {0x1.3755be0000000p-1f, -0x1.14b0ee0000000p-57f, 0x1.fd64ef2361583p-2},
+    {0x1.35dce60000000p-1f, 0x1.9a0dd40000000p-57f, 0x1.011fab085ff8ap-1},
+    {0x1.34679a0000000p-1f, 0x1.7eeaf00000000p-55f, 0x1.0389f052e6342p-1},
+    {0x1.32f5ce0000000p-1f, -0x1.16a9000000000p-56f, 0x1.05f14d38645a4p-1},
+    {0x1.3187760000000p-1f, -0x1.bf67dc0000000p-55f, 0x1.0855c7c6b4511p-1},
+    {0x1.301c820000000p-1f, -0x1.d9d9080000000p-57f, 0x1.0ab76d0ee14d7p-1},
+    {0x1.2eb4ea0000000p-1f, 0x1.c28cae0000000p-58f, 0x1.0d163d019d6b8p-1},
+    {0x1.2d50a00000000p-1f, 0x1.7a84440000000p-55f, 0x1.0f7241e9b497dp-1},
+    {0x1.2bef980000000p-1f, -0x1.79c7720000000p-55f, 0x1.11cb83007cd02p-1},
+    {0x1.2a91ca0000000p-1f, -0x1.d6c3a60000000p-56f, 0x1.142200ec43d4dp-1},
+    {0x1.2937260000000p-1f, -0x1.1699c20000000p-56f, 0x1.1675ca44ba60fp-1},
+    {0x1.27dfa40000000p-1f, -0x1.a835da0000000p-55f, 0x1.18c6e0335cf09p-1},
+    {0x1.268b380000000p-1f, 0x1.a3b8520000000p-55f, 0x1.1b154affda29fp-1},
+    {0x1.2539d80000000p-1f, 0x1.0a75640000000p-56f, 0x1.1d610fbe77003p-1},
+    {0x1.23eb7a0000000p-1f, -0x1.1b21260000000p-56f, 0x1.1faa33be70950p-1},
+    {0x1.22a0120000000p-1f, 0x1.bb587a0000000p-56f, 0x1.21f0c0105beecp-1},
+    {0x1.2157980000000p-1f, -0x1.cebb8c0000000p-57f, 0x1.2434b6fc83934p-1},
+    {0x1.2012020000000p-1f, 0x1.e0eb400000000p-55f, 0x1.26761e85430e9p-1},
+    {0x1.1ecf440000000p-1f, 0x1.2d09fa0000000p-55f, 0x1.28b5007b60783p-1},
+    {0x1.1d8f560000000p-1f, -0x1.30fe6c0000000p-55f, 0x1.2af15fd0640b0p-1},
+    {0x1.1c52300000000p-1f, 0x1.bee9d20000000p-55f, 0x1.2d2b3fa2edc9ep-1},
+    {0x1.1b17c60000000p-1f, 0x1.a074380000000p-55f, 0x1.2f62aa7b09549p-1},
+    {0x1.19e0120000000p-1f, 0x1.8e69120000000p-58f, 0x1.3197a0487fe6cp-1},
+    {0x1.18ab080000000p-1f, 0x1.c46ba60000000p-55f, 0x1.33ca2c0b28995p-1},
+    {0x1.1778a20000000p-1f, 0x1.ff7ea00000000p-55f, 0x1.35fa4e1336ea2p-1},
+    {0x1.1648d60000000p-1f, -0x1.4f1bee0000000p-55f, 0x1.38280e2b8798bp-1},
+    {0x1.151b9a0000000p-1f, 0x1.98b08a0000000p-55f, 0x1.3a53745debdfap-1},
+    {0x1.13f0e80000000p-1f, 0x1.497f4a0000000p-56f, 0x1.3c7c81877320fp-1},
+    {0x1.12c8b80000000p-1f, -0x1.19321c0000000p-56f, 0x1.3ea33a5eb2f61p-1},
+    {0x1.11a3020000000p-1f, 0x1.5ab9140000000p-55f, 0x1.40c7a3ca0dcebp-1},
+    {0x1.107fbc0000000p-1f, 0x1.93bee40000000p-55f, 0x1.42e9c6a1f80bfp-1},
+    {0x1.0f5ee00000000p-1f, -0x1.fc07640000000p-57f, 0x1.4509a4733bb0cp-1},
+    {0x1.0e40660000000p-1f, 0x1.76f66e0000000p-55f, 0x1.472742b53aab3p-1},
+    {0x1.0d24460000000p-1f, -0x1.92ced00000000p-57f, 0x1.4942a7102fc0dp-1},
+    {0x1.0c0a780000000p-1f, -0x1.1e810c0000000p-61f, 0x1.4b5bd75d6e276p-1},
+    {0x1.0af2f80000000p-1f, 0x1.00d4bc0000000p-55f, 0x1.4d72d1fb9fd0bp-1},
+    {0x1.09ddba0000000p-1f, 0x1.cdd5de0000000p-57f, 0x1.4f87a4c3026ebp-1},
+    {0x1.08cabc0000000p-1f, -0x1.a3ce000000000p-55f, 0x1.519a4a87a3450p-1},
+    {0x1.07b9f20000000p-1f, 0x1.dceeb00000000p-56f, 0x1.53aad18999b82p-1},
+    {0x1.06ab5a0000000p-1f, -0x1.9b34360000000p-59f, 0x1.55b934dd40bcep-1},
+    {0x1.059eea0000000p-1f, -0x1.dd13a40000000p-55f, 0x1.57c57f416f191p-1},
+    {0x1.04949c0000000p-1f, -0x1.c3ca1e0000000p-56f, 0x1.59cfb3dbae887p-1},
+    {0x1.038c6c0000000p-1f, 0x1.f8e3640000000p-55f, 0x1.5bd7d20271c77p-1},
+    {0x1.0286500000000p-1f, 0x1.d9f46e0000000p-56f, 0x1.5ddde50149924p-1},
+    {0x1.0182440000000p-1f, 0x1.5e74960000000p-55f, 0x1.5fe1ec791891ep-1},
+    {0x1.0080400000000p-1f, -0x1.436e500000000p-56f, 0x1.61e3f01a46467p-1},
+};
+// ---- END GENERATED SP TABLE ----
+#if PL_SP_FORM == 3
+__shared__ SpCell sp_tab[128];
+#endif
+__device__ __forceinline__ void sp_load_tables(int tid, int nthreads) {
+#if PL_SP_FORM == 3
+    for (int i = tid; i < 128; i += nthreads) sp_tab[i] = kSpLogTab[i];
+    __syncthreads();
+#else
+    (void)tid;
+    (void)nthreads;
+#endif
+}
+#if PL_SP_FORM == 3
+__device__ __forceinline__ double pm_log_t(double y) {  // y >= 1, finite
+    constexpr double kLn2Hi = 0x1.62e42fefa39efp-1, kLn2Lo = 0x1.abc9e3b39803fp-56;
+    const unsigned long long b = (unsigned long long)__double_as_longlong(y);
+    const uint32_t hi_w = (uint32_t)(b >> 32);
+    const int e = __builtin_amdgcn_frexp_exp(y) - 1;  // y = 2^e m, m in [1, 2)
+    const uint32_t j = (hi_w >> 13) & 127u;
+    const double m = __longlong_as_double(
+        (long long)(((unsigned long long)((hi_w & 0x000FFFFFu) | 0x3FF00000u) << 32) | (b & 0xffffffffull)));
+    const SpCell cell = sp_tab[j];
+    const double r = __builtin_fma(m, (double)cell.c, -1.0);
+    const double r2 = r * r;
+    double q = __builtin_fma(-1.0 / 8.0, r, 1.0 / 7.0);
+    q = __builtin_fma(q, r, -1.0 / 6.0);
+    q = __builtin_fma(q, r, 1.0 / 5.0);
+    q = __builtin_fma(q, r, -1.0 / 4.0);
+    q = __builtin_fma(q, r, 1.0 / 3.0);
+    q = __builtin_fma(q, r, -0.5);
+    const double l1 = __builtin_fma(r2, q, r);  // log1p(r)
+    const double de = (double)e;
+    const double h = __builtin_fma(de, kLn2Hi, cell.hi);
+    const double lo = __builtin_fma(de, kLn2Lo, (double)cell.lo) + l1;
+    return h + lo;
+}
+#endif
+
 #if PL_SP_FORM == 0
 __device__ __forceinline__ double softplus_pm(double z) { return pm_log(1.0 + pm_exp(z)); }
+#elif PL_SP_FORM == 3
+__device__ __forceinline__ double softplus_pm(double z) { return pm_log_t(1.0 + pm_exp_e<true>(z)); }
 #else
 __device__ __forceinline__ double softplus_pm(double z) {
     return pm_log_e<PL_SP_FORM == 2>(1.0 + pm_exp_e<PL_SP_FORM == 2>(z));
