@@ -374,6 +374,16 @@ __device__ __forceinline__ void load_tables(int tid, int nthreads) {
     __syncthreads();
 }
 
+// PL_EXF_LEAN (round 4): exp takes 2^(j/128) as one fp64 value (T + T q, not T_hi + (T_lo + T_hi q)),
+// log drops the low part of -ln c_j, and the f builds e^(xc+yc) from the two exps it evaluates
+// anyway -- e^x e^y e^d, d = fl(xc + yc) - (xc + yc) exact in fp64, e^d = 1 + d + d^2/2 (|d| <=
+// 2^-17) -- instead of a third exp: ~13 fewer VALU per f.  Each value's fp64 error grows from
+// ~2^-53 to ~3 2^-53 relative before the one rounding to fp32; the host harness
+// (tools/micro/exactf_rounding.cpp) finds 0 of 5e7 exp, log and f results changed against
+// correctly rounded ones, as before.
+#ifndef PL_EXF_LEAN
+#define PL_EXF_LEAN 1
+#endif
 // e^x in fp64 for fp32 x, |x| <= 200: N = rint(x 128/ln2) by the 1.5 * 2^52 shifter (its low word
 // is N), r = x - N ln2/128 (|r| <= ln2/256, exact to ~2^-60), e^r - 1 = q by a degree-5 Taylor
 // polynomial (remainder < 2^-60), e^x = 2^(N >> 7) T (1 + q), T = 2^((N & 127) / 128) from the
@@ -391,13 +401,27 @@ __device__ __forceinline__ double exp_d(float xf) {
     h = __builtin_fma(h, r, 0.5);
     const double q = __builtin_fma(r2, h, r);
     const int j = n & 127;
+#if PL_EXF_LEAN
+    const double th = tabs.e[2 * j];
+    const double m = __builtin_fma(th, q, th);
+#else
     const double th = tabs.e[2 * j], tl = tabs.e[2 * j + 1];
     const double m = __builtin_fma(th, q, tl) + th;
+#endif
     return __builtin_ldexp(m, n >> 7);
 }
 // fp32 exp(x), |x| <= 87, correctly rounded (but for ~2^-28 of the arguments): one rounding of
 // the fp64 value (the 2^k scaling is exact in fp64)
 __device__ __forceinline__ float exp_cr(float xf) { return (float)exp_d(xf); }
+// fp32 e^(fl(xc + yc)) from the fp64 e^xc, e^yc: e^xc e^yc e^d, d = fl(xc + yc) - (xc + yc), which
+// Fast2Sum gives exactly in fp32 ((s - a) - b with |a| >= |b|)
+__device__ __forceinline__ float exp_sum(double ex, double ey, float xc, float yc) {
+    const float s = xc + yc;
+    const bool sw = __builtin_fabsf(yc) > __builtin_fabsf(xc);
+    const float a = sw ? yc : xc, b = sw ? xc : yc;
+    const double d = (double)((s - a) - b);
+    return (float)(ex * ey * __builtin_fma(d, __builtin_fma(d, 0.5, 1.0), 1.0));
+}
 
 // ln x in fp64 for normal fp32 x > 0: d = bits(x) - bits(sqrt(1/2)), e = d >> 23 (arithmetic),
 // m = 2^-e x in [sqrt(1/2), sqrt(2)) (its bits: the low 23 of d + bits(sqrt(1/2))), cell j = bits
@@ -419,7 +443,11 @@ __device__ __forceinline__ double log_d(float xf) {
     const double l1 = __builtin_fma(r2, p, r);
     const double de = (double)e;
     const double hi = __builtin_fma(de, kTabLn2Hi, tabs.l[2 * j]);
+#if PL_EXF_LEAN
+    const double lo = __builtin_fma(de, kTabLn2Lo, l1);
+#else
     const double lo = __builtin_fma(de, kTabLn2Lo, tabs.l[2 * j + 1]) + l1;
+#endif
     return hi + lo;
 }
 __device__ __forceinline__ float log_cr(float xf) { return (float)log_d(xf); }
@@ -461,8 +489,14 @@ constexpr float kExactFastLmax = 43.0f;
 __device__ __attribute__((noinline)) float f_exact(float x, float y, float lmax) {
     if (lmax > kExactFastLmax) return f_exact_wide(x, y, lmax);
     const float xc = fminf(fmaxf(x, -lmax), lmax), yc = fminf(fmaxf(y, -lmax), lmax);
+#if PL_EXF_LEAN
+    const double ex = exp_d(xc), ey = exp_d(yc);
+    float o = log_cr(1.0f + exp_sum(ex, ey, xc, yc));
+    o -= log_cr((float)ex + (float)ey);
+#else
     float o = log_cr(1.0f + exp_cr(xc + yc));
     o -= log_cr(exp_cr(xc) + exp_cr(yc));
+#endif
     return o;
 }
 
@@ -476,9 +510,15 @@ __device__ __attribute__((noinline)) f2 f_exact2(float x0, float y0, float x1, f
     if (lmax > kExactFastLmax) return f2{f_exact_wide(x0, y0, lmax), f_exact_wide(x1, y1, lmax)};
     const float xc0 = fminf(fmaxf(x0, -lmax), lmax), yc0 = fminf(fmaxf(y0, -lmax), lmax);
     const float xc1 = fminf(fmaxf(x1, -lmax), lmax), yc1 = fminf(fmaxf(y1, -lmax), lmax);
+#if PL_EXF_LEAN
+    const double ea0 = exp_d(xc0), ea1 = exp_d(xc1), eb0 = exp_d(yc0), eb1 = exp_d(yc1);
+    const float s0 = exp_sum(ea0, eb0, xc0, yc0), s1 = exp_sum(ea1, eb1, xc1, yc1);
+    const float a0 = (float)ea0, a1 = (float)ea1, b0 = (float)eb0, b1 = (float)eb1;
+#else
     const float s0 = exp_cr(xc0 + yc0), s1 = exp_cr(xc1 + yc1);
     const float a0 = exp_cr(xc0), a1 = exp_cr(xc1);
     const float b0 = exp_cr(yc0), b1 = exp_cr(yc1);
+#endif
     const float p0 = log_cr(1.0f + s0), p1 = log_cr(1.0f + s1);
     const float q0 = log_cr(a0 + b0), q1 = log_cr(a1 + b1);
     f2 r;

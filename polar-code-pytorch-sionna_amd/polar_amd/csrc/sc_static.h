@@ -369,9 +369,20 @@ __device__ __attribute__((noinline)) float f_lane_exact(float a, float y, uint32
     const bool A = (int32_t)role31 < 0;
     float arg;
     if constexpr (TOP) {
+#if PL_EXF_LEAN
+        // e^(x+y) from the pair's two fp64 exps (exactf.h exp_sum) instead of a third exp
+        const double ed = plx::exp_d(xc);
+        const unsigned long long eb = (unsigned long long)__double_as_longlong(ed);
+        const uint32_t plo = mir<S>((uint32_t)eb), phi = mir<S>((uint32_t)(eb >> 32));
+        const double edp = __longlong_as_double((long long)(((unsigned long long)phi << 32) | plo));
+        const float e = (float)ed;
+        const float es = e + (float)edp;  // e^x + e^y in both lanes of the pair
+        const float e1 = plx::exp_sum(ed, edp, xc, yc);
+#else
         const float e = plx::exp_cr(xc);
         const float es = e + mirf<S>(e);  // e^x + e^y in both lanes of the pair
         const float e1 = plx::exp_cr(xc + yc);
+#endif
         arg = A ? 1.0f + e1 : es;
     } else {
         const float e = plx::exp_cr(A ? xc + yc : xc);
