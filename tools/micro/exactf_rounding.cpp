@@ -12,23 +12,21 @@
 
 #include "exactf_tables.inc"
 
-static double exp_d(float xf) {  // exactf.h exp_d
+static double exp_d(float xf) {  // exactf.h exp_d (PL_EXF_LEAN: 2^(j/256) one-part, degree 4)
     const double x = xf;
-    const double t = fma(x, kTabInvC, 0x1.8p52);
+    const double t = fma(x, kTabInvC1, 0x1.8p52);
     uint64_t tb;
     memcpy(&tb, &t, 8);
     const int n = (int)(uint32_t)tb;
     const double nd = t - 0x1.8p52;
-    double r = fma(-nd, kTabCHi, x);
-    r = fma(-nd, kTabCLo, r);
+    double r = fma(-nd, kTabC1Hi, x);
+    r = fma(-nd, kTabC1Lo, r);
     const double r2 = r * r;
-    double h = fma(1.0 / 120.0, r, 1.0 / 24.0);
-    h = fma(h, r, 1.0 / 6.0);
+    double h = fma(1.0 / 24.0, r, 1.0 / 6.0);
     h = fma(h, r, 0.5);
     const double q = fma(r2, h, r);
-    const int j = n & 127;
-    const double m = fma(kTabExp[2 * j], q, kTabExp[2 * j]);  // PL_EXF_LEAN: one-part 2^(j/128)
-    return ldexp(m, n >> 7);
+    const double th = kTabExp1[n & 255];
+    return ldexp(fma(th, q, th), n >> 8);
 }
 static double log_d(float xf) {  // exactf.h log_d
     uint32_t b;
