@@ -243,6 +243,10 @@ __device__ __forceinline__ float fop(float x, float y, float lmax) {
 #ifndef PL_SC_FEX_LANE
 #define PL_SC_FEX_LANE 1  // exact f of lane-level nodes split over the lanes holding the pair (f_lane_exact)
 #endif
+#ifndef PL_SC_G_NODPP
+#define PL_SC_G_NODPP 0  // 1: lane-level g as two flips and a plain add, no DPP read of a fresh value and
+                         // no hazard s_nop (A/B r04zl, (512,1024): 1.3 % slower)
+#endif
 template <int FM, bool BND, int H>
 __device__ __forceinline__ void fvec(const float* a, float* x, float lmax) {
     if constexpr (FM == 1 && H >= 2 && PL_SC_FEX_PAIR) {
@@ -420,8 +424,16 @@ __device__ __forceinline__ uint32_t lsplit(float a, const Lane& ln) {
     // both lanes of the pair evaluate (1-2u) alpha_lo + alpha_hi: the low lane flips its own
     // value (bitop3 S1 ^ (S0 & S2) with the lane's bit-31 mask), the high lane keeps its own, and
     // one DPP add sums the pair in both lanes (fp32 addition is commutative: same bits)
+#if PL_SC_G_NODPP
+    // the same sum without reading the just-flipped value across lanes (no DPP hazard wait): the
+    // low lane flips its own value, the high lane the partner's copy y (taken before the left
+    // subtree), and both add -- the same two operands, so the same bits
+    const float x = uf(__builtin_amdgcn_bitop3_b32(bl, fu(a), ln.lo31[s], 0x6c)) +
+                    uf(__builtin_amdgcn_bitop3_b32(bl, fu(y), ln.lo31[s] ^ 0x80000000u, 0x6c));
+#else
     const float v = uf(__builtin_amdgcn_bitop3_b32(bl, fu(a), ln.lo31[s], 0x6c));
     const float x = v + mirf<S>(v);
+#endif
     const uint32_t br = lnode<C, s - 1, P + S / 2>(x, ln);
     return __builtin_amdgcn_bitop3_b32(bl, br, ln.lo31[s], 0x6c);  // br ^ (bl & lo31)
 #else
