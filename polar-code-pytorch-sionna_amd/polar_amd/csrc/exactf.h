@@ -427,21 +427,34 @@ __device__ const double kTabLogL[512] = {
 #ifndef PL_EXF_LEAN
 #define PL_EXF_LEAN 1
 #endif
-// LDS copies of the tables, one per work-group (8 KiB): every kernel that evaluates the exact f
+// LDS copies of the tables, one per work-group (6 KiB lean, 8 KiB otherwise): every kernel that evaluates the exact f
 // calls load_tables() before its first f (all threads of the work-group, then a barrier).
+#if PL_EXF_LEAN
+struct alignas(16) Tabs {
+    double e[256];   // kTabExp1
+    double cl[512];  // cell j: {c_j, hi(-ln c_j)} side by side, one 16-byte read (6 KiB in all)
+};
+#else
 struct alignas(16) Tabs {
     double e[256];  // kTabExp
     double c[256];  // kTabLogC
     double l[512];  // kTabLogL
 };
+#endif
 __shared__ Tabs tabs;
 
 __device__ __forceinline__ void load_tables(int tid, int nthreads) {
     for (int i = tid; i < 256; i += nthreads) {
-        tabs.e[i] = PL_EXF_LEAN ? kTabExp1[i] : kTabExp[i];
+#if PL_EXF_LEAN
+        tabs.e[i] = kTabExp1[i];
+        tabs.cl[2 * i] = kTabLogC[i];
+        tabs.cl[2 * i + 1] = kTabLogL[2 * i];
+#else
+        tabs.e[i] = kTabExp[i];
         tabs.c[i] = kTabLogC[i];
         tabs.l[i] = kTabLogL[i];
         tabs.l[i + 256] = kTabLogL[i + 256];
+#endif
     }
     __syncthreads();
 }
@@ -515,7 +528,12 @@ __device__ __forceinline__ double log_d(float xf) {
     const uint32_t mb = (uint32_t)d & 0x7FFFFFu;
     const int j = (int)(mb >> 15);
     const double m = (double)__uint_as_float(mb + kTabLogBase);
+#if PL_EXF_LEAN
+    const double2 cl = *reinterpret_cast<const double2*>(&tabs.cl[2 * j]);
+    const double r = __builtin_fma(m, cl.x, -1.0);
+#else
     const double r = __builtin_fma(m, tabs.c[j], -1.0);
+#endif
     const double r2 = r * r;
     double p = __builtin_fma(-1.0 / 6.0, r, 1.0 / 5.0);
     p = __builtin_fma(p, r, -0.25);
@@ -523,10 +541,11 @@ __device__ __forceinline__ double log_d(float xf) {
     p = __builtin_fma(p, r, -0.5);
     const double l1 = __builtin_fma(r2, p, r);
     const double de = (double)e;
-    const double hi = __builtin_fma(de, kTabLn2Hi, tabs.l[2 * j]);
 #if PL_EXF_LEAN
+    const double hi = __builtin_fma(de, kTabLn2Hi, cl.y);
     const double lo = __builtin_fma(de, kTabLn2Lo, l1);
 #else
+    const double hi = __builtin_fma(de, kTabLn2Hi, tabs.l[2 * j]);
     const double lo = __builtin_fma(de, kTabLn2Lo, tabs.l[2 * j + 1]) + l1;
 #endif
     return hi + lo;
