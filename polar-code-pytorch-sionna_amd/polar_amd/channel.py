@@ -27,6 +27,15 @@ def ebnodb2no(ebno_db, n_bits_per_sym, coderate):
     return 1 / (ebno * coderate * n_bits_per_sym / 1)
 
 
+def splitmix64(x):
+    """splitmix64's finaliser (Steele, Lea, Flood 2014): a bijection of 64-bit words."""
+    m = 2 ** 64 - 1
+    z = x & m
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+    return z ^ (z >> 31)
+
+
 def _qam_points(n_bits_per_sym):
     """Gray-labelled, unit-energy QAM points as complex64 numpy (mapping.py:7-48 arithmetic)."""
     assert n_bits_per_sym % 2 == 0 and n_bits_per_sym > 0
@@ -208,7 +217,8 @@ class FusedAWGN(nn.Module):
     stream=(point, iteration) (sim_ber passes its loop indices, so a speculatively launched
     iteration never shifts another point's codewords); without it every call draws the next
     iteration of point 0 (`iteration` counts those calls).  The key is `seed` in the first run and
-    changes with every run sim_ber makes over the model (`epoch`, next_epoch()).  Stream row r of a draw is codeword
+    changes with every run sim_ber makes over the model (`epoch`, next_epoch(): sim_ber mutates the model it is
+    given, once per call, also when the call raises).  Stream row r of a draw is codeword
     row0 + r; the point lives in the row's high 32 bits (counter word 1), so row0 + batch_size
     must stay below 2^32.  `row0` offsets the rows (a rank's shard of a multi-GPU batch)."""
 
@@ -241,9 +251,13 @@ class FusedAWGN(nn.Module):
         self.epoch += 1
 
     def key(self):
-        """The Philox key of the current epoch: the seed itself in epoch 0, otherwise the seed
-        XOR a Weyl multiple of the epoch (distinct keys for distinct epochs of one seed)."""
-        return (self.seed ^ (self.epoch * 0x9E3779B97F4A7C15)) & (2 ** 64 - 1)
+        """The Philox key of the current epoch: the seed itself in epoch 0 (the pinned streams),
+        otherwise splitmix64(seed + epoch * golden gamma) -- a bijective mixer, so distinct epochs
+        of one seed get distinct keys, and related seeds (seed vs seed ^ gamma) do not replay each
+        other's epochs the way a plain seed ^ epoch * gamma key would."""
+        if self.epoch == 0:
+            return self.seed & (2 ** 64 - 1)
+        return splitmix64((self.seed + self.epoch * 0x9E3779B97F4A7C15) & (2 ** 64 - 1))
 
     def _make_plan(self, dev):
         from . import _lib

@@ -1493,7 +1493,9 @@ __device__ __forceinline__ void decode_staged(const float* __restrict__ llr, int
     ln.lom_[0] = 0u;
 #endif
     ln.lmax = lmax;
-    if constexpr (C::FM == 1) plx::load_tables(threadIdx.x, blockDim.x);
+    // exact f would add the tables' LDS object next to the single Staged array (see above: the
+    // compiler may then drain the copies early); the staged kernel is a rejected min-sum A/B
+    static_assert(C::FM == 0, "PL_SC_PERSIST == 2 (staged kernel): min-sum codes only");
     uint32_t* ubase = lds + wave * 64 * WPL;
     uint32_t* mine = lds + (wave * 64 + lane) * WPL;
     float* rows = reinterpret_cast<float*>(lds + S::U_WORDS) + wave * CW * S::ROW;

@@ -608,15 +608,16 @@ __device__ __forceinline__ void vlev_shared(double* vx, double* vy, double lmax)
 // The stage-7 cache at L <= 8 only: the wider lists' kernels spill with it (L = 16: 38 VGPRs).
 template <int L, int FM>
 constexpr bool c7_on() { return PL_SCL_C7 && FM == 0 && L <= 8; }
+constexpr int kVcEntries = 32;  // (item, path) entries per lane: IT * L <= 32 (node_fg checks it)
 template <int FM>
 struct VCache {
-    double2 v[32];   // [it * L + path]: (x, y) = stage-6 elements (j, j + 32); IT * L <= 32
+    double2 v[kVcEntries];   // [it * L + path]: (x, y) = stage-6 elements (j, j + 32); IT * L <= 32
 };
 template <>
 struct VCache<0> {  // min-sum
-    double2 v[32];
+    double2 v[kVcEntries];
 #if PL_SCL_C7
-    double4 v7[32];  // the stage-7 elements (j, j + 64 | j + 32, j + 96) of the same path
+    double4 v7[kVcEntries];  // the stage-7 elements (j, j + 64 | j + 32, j + 96) of the same path
     int p7;          // start of the stage-7 node v7 belongs to (fast-SCL may prune the left pass
                      // that writes it: the right child's pass then recomputes); same in every lane
 #endif
@@ -766,6 +767,7 @@ __device__ __forceinline__ void vnode64_c7(const St& t, const Cw& w, int j, int 
 template <int L, int V, int NS, int FM, int CPW>
 __device__ void vvisit64(const St& t, int pos, bool is_g, int lane, const int* wb, uint32_t gmask, VCache<FM>* vc) {
     constexpr int NC = 1 << V, ls = 5, h = 32, hs = 64;
+    static_assert((CPW * h + 63) / 64 * L <= kVcEntries, "VCache: items per lane x paths");
     if (vc != nullptr && is_g) {
 #if PL_SCL_VC_BATCH
 #pragma unroll
@@ -1143,6 +1145,15 @@ template <int L, int V, int FM, int CPW>
 __device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane, VCache<FM>* vc) {
     constexpr int LL = ilog2(L);
     const int ls = s - 1, h = 1 << ls;
+    // the per-lane cache holds kVcEntries (item, path) entries.  Release builds run pick_v's V,
+    // whose virtual nodes have h <= 32 (S = 10: V = 4; S = 9: V = 3; below: h = 16), i.e. at most
+    // CPW * 32 / 64 * L = 16 entries.  Development builds can put larger nodes on the virtual path
+    // (PL_SCL_VIRTUAL below pick_v's V): such a pass runs uncached -- the left and right passes of
+    // a node share h, so both see the same decision.  (A runtime check in release builds changed
+    // the exact-f kernels' register allocation: 84 VGPR spills.)
+#if PL_DEV
+    if (vc != nullptr && ((CPW * h + 63) / 64) * L > kVcEntries) vc = nullptr;
+#endif
     if (PL_SCL_DIAG_SKIP_V && s > t.SS) {
     } else if (PL_SCL_DIAG_SKIP_ST && s <= t.SS) {
     } else if (PL_SCL_ST_UNROLL && FM == 0 && s <= t.SS && ls <= R + 1) {  // exact f: spills (7.7 -> 11.2 ms)

@@ -95,48 +95,51 @@ def sim_ber(mc_fun, ebno_dbs, batch_size, max_mc_iter, soft_estimates=False, tar
     status = tc.zeros(P)
     runtime = np.zeros(P)
     header_done = False
-    for i in range(P):
-        t0 = time.perf_counter()
-        done, w, stop, it = 0, 0, False, -1
-        while done < max_mc_iter and not stop:
-            w = _next_window(w, done, max_mc_iter, cnt[i], target_bit_errs, target_block_errs, wmax)
-            block = _run_window(mc_fun, model, fused, keyed, i, done, w, batch_size, ebno_dbs[i], soft_estimates)
-            block = block.to(cdev)
-            if dist is not None:
-                dist.all_reduce(block, op=dist.ReduceOp.SUM, group=process_group)
-            host = block.cpu().numpy()  # one host sync per window (the reference: per iteration, sim.py:114)
-            for j in range(w):
-                it = done + j
-                cnt[i] += host[j]
-                if verbose:
-                    if not header_done:
-                        _row(_HEADER, "\n")
-                        print('-' * 135)
-                        header_done = True
-                    _row(_cells(ebno_dbs[i], cnt[i], time.perf_counter() - t0, f"iter: {it:.0f}/{max_mc_iter:.0f}"), "\r")
-                if target_bit_errs is not None and cnt[i, 0] >= target_bit_errs:
-                    status[i] = 3
-                    stop = True
-                    break
-                if target_block_errs is not None and cnt[i, 1] >= target_block_errs:
-                    status[i] = 4
-                    stop = True
-                    break
-                if it == max_mc_iter - 1:
-                    status[i] = 1
-            done += w
-        runtime[i] = time.perf_counter() - t0
-        if verbose:
-            _row(_cells(ebno_dbs[i], cnt[i], runtime[i], _STATUS[int(status[i])]), "\n")
-        if early_stop and cnt[i, 1] == 0:
-            status[i] = 2
+    try:
+        for i in range(P):
+            t0 = time.perf_counter()
+            done, w, stop, it = 0, 0, False, -1
+            while done < max_mc_iter and not stop:
+                w = _next_window(w, done, max_mc_iter, cnt[i], target_bit_errs, target_block_errs, wmax)
+                block = _run_window(mc_fun, model, fused, keyed, i, done, w, batch_size, ebno_dbs[i], soft_estimates)
+                block = block.to(cdev)
+                if dist is not None:
+                    dist.all_reduce(block, op=dist.ReduceOp.SUM, group=process_group)
+                host = block.cpu().numpy()  # one host sync per window (the reference: per iteration, sim.py:114)
+                for j in range(w):
+                    it = done + j
+                    cnt[i] += host[j]
+                    if verbose:
+                        if not header_done:
+                            _row(_HEADER, "\n")
+                            print('-' * 135)
+                            header_done = True
+                        _row(_cells(ebno_dbs[i], cnt[i], time.perf_counter() - t0, f"iter: {it:.0f}/{max_mc_iter:.0f}"), "\r")
+                    if target_bit_errs is not None and cnt[i, 0] >= target_bit_errs:
+                        status[i] = 3
+                        stop = True
+                        break
+                    if target_block_errs is not None and cnt[i, 1] >= target_block_errs:
+                        status[i] = 4
+                        stop = True
+                        break
+                    if it == max_mc_iter - 1:
+                        status[i] = 1
+                done += w
+            runtime[i] = time.perf_counter() - t0
             if verbose:
-                print(f"\nSimu stopped as no error occurred @ EbNo = {ebno_dbs[i].numpy():.1f} dB.\n")
-            break
-    # the next run draws fresh codewords (keyed models: a new epoch of the (point, iteration) key)
-    next_epoch = getattr(model, "next_epoch", None)
-    if callable(next_epoch):
-        next_epoch()
+                _row(_cells(ebno_dbs[i], cnt[i], runtime[i], _STATUS[int(status[i])]), "\n")
+            if early_stop and cnt[i, 1] == 0:
+                status[i] = 2
+                if verbose:
+                    print(f"\nSimu stopped as no error occurred @ EbNo = {ebno_dbs[i].numpy():.1f} dB.\n")
+                break
+    finally:
+        # the next run draws fresh codewords (keyed models: a new epoch of the (point, iteration)
+        # key) -- also after a run that raised or was interrupted, so a retry never redraws it
+        next_epoch = getattr(model, "next_epoch", None)
+        if callable(next_epoch):
+            next_epoch()
     c = tc.from_numpy(cnt)
     ber = c[:, 0] / c[:, 2]
     bler = c[:, 1] / c[:, 3]

@@ -57,7 +57,10 @@ def _scl_l8_asm():
     return _SCL_ASM["asm"]
 
 
-def test_scl_bench_kernel_has_no_spills_or_scratch():
+def test_scl_bench_kernel_no_vgpr_spills_private_memory_is_the_vcache():
+    """No VGPR spills.  Private memory (scratch) IS used: the per-lane virtual-node cache (VCache,
+    stage-6 and stage-7 entries, <= 1616 B with the frame) lives there by design; the bound below
+    is what this test permits."""
     asm = _scl_l8_asm()
     # scl_tree_kernel<L = 8, V = 4, f_mode = 0 (min-sum), FAST = false>: the kernel bench.py --decoder scl runs
     meta = _kernel_meta(asm, lambda n: "scl_tree_kernelILi8ELi4ELi0ELb0E" in n)
@@ -186,3 +189,23 @@ def test_bench_kernel_instruction_streams_are_pinned():
     got = current_pins()
     for key in got:
         assert got[key] == want[key], (key, got[key], want[key], "re-pin with: python tools/pin_isa.py")
+
+
+def test_scl_vcache_entries_fit_for_release_virtual_stages():
+    """the per-lane VCache has kVcEntries = 32 (item, path) entries.  Every release
+    configuration (pick_v's V for n = 32 ... 1024, L = 2 ... 32) needs at most that many; larger
+    virtual nodes exist only in development builds, where node_fg runs them uncached."""
+    R = 4
+    for S in range(5, 11):
+        v = min(S - 1 - R, 4)
+        if v == 4 and S != 10:
+            v = 3
+        v = max(v, 0)
+        if v == 0:
+            continue
+        h = 1 << (S - 1 - v)  # elements per half of the first virtual node (stage SS + 1)
+        for L in (2, 4, 8, 16, 32):
+            cpw = 32 // L
+            assert (cpw * h + 63) // 64 * L <= 32, (S, v, L)
+    src = open(os.path.join(_build.CSRC, "scl_tree_kernel.hip")).read()
+    assert "constexpr int kVcEntries = 32;" in src

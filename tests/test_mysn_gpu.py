@@ -72,8 +72,8 @@ def test_mysn_scl_random_code_vs_oracle(pa, log_n, L, fast):
     move by one ulp, and 0-1 of 37 on these codes.)"""
     from polar_amd import _lib, ops
     n = 1 << log_n
-    if n * L > 4096:
-        pytest.skip("oracle time")
+    # every shape runs, n = 1024 at L = 8 included (the configs[3] shape, with and without fast-SCL):
+    # the C oracle decodes these 37 rows in ~0.03 s
     rng = np.random.default_rng(log_n * 7 + L + fast)
     k = n // 2
     fp = np.sort(rng.permutation(n)[: n - k])

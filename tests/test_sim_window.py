@@ -196,3 +196,29 @@ def test_counter_device_follows_the_group_backend():
     assert sim._counter_device("cpu", None, None, M()) == tc.device("cpu")
     assert sim._counter_device("cpu", FakeDist("nccl"), None, M()) == tc.device("cuda", 3)
     assert sim._counter_device("cuda", FakeDist("gloo"), None, M()) == tc.device("cpu")
+
+
+def test_epoch_keys_mix_and_interrupted_runs_advance():
+    """epoch keys come from a mixing function (related seeds do not replay each other's
+    epochs), and a sim_ber run that raises still advances the epoch (a retry draws fresh codewords)."""
+    from polar_amd import channel, frozen, sim
+    C = 0x9E3779B97F4A7C15
+    fp = frozen.reference_frozen_pos(32, 64)
+    a = channel.FusedAWGN(64, 32, fp, None, device="cpu", seed=42)
+    b = channel.FusedAWGN(64, 32, fp, None, device="cpu", seed=42 ^ ((1 * C) ^ (2 * C)))
+    a.epoch, b.epoch = 2, 1  # the XOR key gave (seed, 2) and (seed ^ (C ^ 2C), 1) the same key
+    assert a.key() != b.key()
+    keys = {channel.FusedAWGN(64, 32, fp, None, device="cpu", seed=s).key() for s in range(50)}
+    assert len(keys) == 50  # epoch 0: the seed itself
+
+    class Boom(channel.FusedAWGN):
+        def error_counts(self, batch_size, ebno_db, counts=None, stream=None):
+            return None
+
+        def forward(self, batch_size, ebno_db, stream=None):
+            raise KeyboardInterrupt
+
+    m = Boom(64, 32, fp, None, device="cpu", seed=7)
+    with pytest.raises(KeyboardInterrupt):
+        sim.sim_ber(m, [1.0], 4, max_mc_iter=2, verbose=False)
+    assert m.epoch == 1 and m.key() != 7

@@ -25,21 +25,29 @@ def main():
     mask = polar_amd.frozen_mask(fp, a.n)
     g = torch.Generator(device="cuda").manual_seed(5)
     llr = (torch.randn((a.bs, a.n), device="cuda", generator=g) * 2.5 + 1.0).contiguous()
+    sys.path.insert(0, ROOT)
+    from bench import _time_launches  # the bench's launch sequence (configs_3 of the JSON line)
     for name, fm, flags in (("minsum", 0, 0), ("exact", 1, 0), ("minsum+fast", 0, _lib.PL_PLAN_FAST_SCL),
                             ("exact+fast (my_sn default)", 1, _lib.PL_PLAN_FAST_SCL)):
         plan = _lib.Plan(a.n, mask, a.L, fm, flags=flags)
         out = torch.empty((a.bs, a.k), device="cuda")
-        ops.scl_decode(plan, llr, out=out)
+        ws = ops.scl_workspace(plan, a.bs, llr.device)
+        fn = lambda: ops.scl_decode(plan, llr, out=out, workspace=ws)  # noqa: E731
+        fn()
         torch.cuda.synchronize()
+        # cold: 3 launches right after the first (what this tool reported until round 4: the GPU
+        # clock has not left its idle state yet, and the module path allocated the workspace per call)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(3):
             ops.scl_decode(plan, llr, out=out)
         e1.record()
         torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1) / 3
-        print(f"{name:28s} kernel={plan.kernel()[0]:12s} {ms:8.3f} ms  {a.bs / ms / 1e3:7.4f} Mcw/s", flush=True)
-
+        cold = e0.elapsed_time(e1) / 3
+        # settled: bench.py's sequence (50 ms of untimed launches, 3 warm-up, 20 timed)
+        ms = _time_launches(fn, 20, 3, 50.0, llr.device)
+        print(f"{name:28s} kernel={plan.kernel()[0]:12s} {ms:8.3f} ms  {a.bs / ms / 1e3:7.4f} Mcw/s"
+              f"  (cold, 3 launches, workspace per call: {cold:.3f} ms)", flush=True)
 
 if __name__ == "__main__":
     main()
