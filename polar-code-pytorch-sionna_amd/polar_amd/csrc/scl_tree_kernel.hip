@@ -153,6 +153,24 @@ constexpr int R = PL_SCL_R;  // stage of the lane-local subtree
 constexpr int T = 1 << R;    // leaves per lane-local subtree (<= one partial-sum word)
 constexpr int SPS = 16;      // bytes per path of the stage-owner table (S + 1 <= 16), one 16-byte row
 
+// Two rows per codeword (X2): the L = 8 min-sum kernel at n = 1024 decodes 2
+// codewords per wave instead of 4, so bs = 8192 gives 4096 waves (4 per SIMD instead of 2).  Each
+// codeword owns two 16-lane DPP rows holding the same 2L candidates; the rows split the lane
+// subtree's stage buffers (row r keeps the elements j = r mod 2 of stages 1..R-1, so every f/g of
+// those stages is row-local and half as long), the 15-rotation rank (row 0 offsets 1..8, row 1
+// offsets 9..15 on a source pre-rotated by 8; one v_permlane16_swap adds the halves) and the moves
+// at a fork (each row pushes its own half of the live buffers).  The leaf value, the metric
+// penalty, the partial sums and the origin are the same in both rows.  The upper stages are
+// wave-parallel loops over (codeword, path, element) and simply run over 2 codewords.
+#ifndef PL_SCL_X2
+#define PL_SCL_X2 0
+#endif
+#ifndef PL_SCL_X2_WPE
+#define PL_SCL_X2_WPE 4  // amdgpu_waves_per_eu of the X2 kernel (4: <= 128 VGPRs, all 4096 waves of bs = 8192 resident)
+#endif
+template <int L, int V, int FM, bool FAST>
+__host__ __device__ constexpr int xrep() { return (PL_SCL_X2 && L == 8 && V == 4 && FM == 0 && !FAST) ? 2 : 1; }
+
 __host__ __device__ constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x >> 1); }
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
 
@@ -398,6 +416,53 @@ __device__ __forceinline__ int rank16_split(double cv) {
 #undef PL_RANK_ROT_A
 #undef PL_RANK_ROT_B
 #endif
+
+// ---- X2 helpers (two rows per codeword) ---------------------------------------------------
+// v_permlane16_swap(v, v) exchanges rows 2c+1 and 2c: the first result holds the even row's value
+// in both rows, the second the odd row's.  e0 / e1 = this double in the even / odd row.
+__device__ __forceinline__ void xch_rows(double v, double& e0, double& e1) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)(b & 0xffffffffull), hi = (unsigned)(b >> 32);
+    const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    e0 = __longlong_as_double((long long)(((unsigned long long)rh[0] << 32) | rl[0]));
+    e1 = __longlong_as_double((long long)(((unsigned long long)rh[1] << 32) | rl[1]));
+}
+__device__ __forceinline__ int sum_rows(int v) {
+    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+    return (int)(r[0] + r[1]);
+}
+// Rank of this lane's candidate among the 16 of its row pair (both rows hold the same 16), the
+// stable (metric, index) order of rank16_subb.  Even rows compare against row offsets 1..8 of the
+// candidates themselves, odd rows against offsets 1..8 of a copy pre-rotated by 8 (offsets 9..16;
+// 16 is the lane itself, tie mask 0, so it counts nothing): 8 borrow-chain rotations per lane
+// instead of 15, and one v_permlane16_swap adds the two rows' counts.  The tie mask of a rotation
+// holds both rows' bits (even: lanes >= d, odd: lanes >= d + 8) in each 32-bit half of VCC.
+#define PL_RANK_ROT_X2(r, m)                                                                \
+    "s_mov_b32 vcc_lo, " #m "\n\t"                                                          \
+    "s_mov_b32 vcc_hi, " #m "\n\t"                                                          \
+    "v_subb_co_u32_dpp %1, vcc, %4, %2, vcc row_ror:" #r " row_mask:0xf bank_mask:0xf\n\t" \
+    "v_subb_co_u32_dpp %1, vcc, %5, %3, vcc row_ror:" #r " row_mask:0xf bank_mask:0xf\n\t" \
+    "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n\t"
+__device__ __forceinline__ int rank16_x2(double cv) {
+    const long long b = __double_as_longlong(cv);
+    const int lo = (int)(b & 0xffffffffLL), hi = (int)(b >> 32);
+    // the comparison source: the candidates themselves in even rows, rotated by 8 in odd rows
+    const int slo = __builtin_amdgcn_update_dpp(lo, lo, 0x128, 0xA, 0xF, false);
+    const int shi = __builtin_amdgcn_update_dpp(hi, hi, 0x128, 0xA, 0xF, false);
+    int rk, tmp;
+    asm volatile(
+        "s_nop 1\n\t"  // the DPP sources were just written by a VALU
+        "v_mov_b32 %0, 0\n\t"
+        PL_RANK_ROT_X2(1, 0xfe00fffe) PL_RANK_ROT_X2(2, 0xfc00fffc) PL_RANK_ROT_X2(3, 0xf800fff8)
+        PL_RANK_ROT_X2(4, 0xf000fff0) PL_RANK_ROT_X2(5, 0xe000ffe0) PL_RANK_ROT_X2(6, 0xc000ffc0)
+        PL_RANK_ROT_X2(7, 0x8000ff80) PL_RANK_ROT_X2(8, 0x0000ff00)
+        : "=&v"(rk), "=&v"(tmp)
+        : "v"(lo), "v"(hi), "v"(slo), "v"(shi)
+        : "vcc");
+    return sum_rows(rk);
+}
+#undef PL_RANK_ROT_X2
 
 template <int GW, int r>
 __device__ __forceinline__ void rank_rot(double cv, int gl, int lane, int& rk) {
@@ -684,6 +749,67 @@ __device__ __forceinline__ void vnode64(const St& t, const Cw& w, const float* c
         w.A[p * t.per + (1 << ls) - (1 << R) + j] = r;
     }
 }
+// vnode64 for NS = 0 (the channel level a g: the passes of the codeword's right half that start
+// from the channel) with one side at a time: the x side of every path (its results kept, one double
+// per path), then the y side and the node's f/g.  The X2 kernel's register budget (128 VGPRs):
+// both sides at once hold 32 channel values and 16 doubles per path step, which spilled.  The same
+// f/g operands and operations per element as vnode64, so the same values.
+template <int Q, int FM>
+__device__ __forceinline__ void vside_levels(double* v, const uint32_t* bp, const int* wb, int j, int side,
+                                             uint32_t gmask, double lmax) {
+    if constexpr (Q >= 0) {
+        constexpr int h = 1 << Q;
+        if ((gmask >> Q) & 1u) {
+            const uint32_t* wq = bp + wb[Q] + side;
+#pragma unroll
+            for (int m = 0; m < h; ++m) v[m] = g_op(v[m], v[m + h], (wq[2 * m] >> j) & 1u);
+        } else {
+#pragma unroll
+            for (int m = 0; m < h; ++m) v[m] = f_op<FM>(v[m], v[m + h], lmax);
+        }
+        vside_levels<Q - 1, FM>(v, bp, wb, j, side, gmask, lmax);
+    }
+}
+template <int L, int V, int FM>
+__device__ __forceinline__ void vnode64_ns0(const St& t, const Cw& w, const float* ch, int co, const int* wb, int j,
+                                            uint32_t gmask, bool is_g, int pos, int ls, VCache<FM>* vc, int it,
+                                            bool w7) {
+    constexpr int H = 1 << (V - 1), NC = 2 * H, hs = 64, h = 32;
+    double xr[L];
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+        float c[NC];
+#pragma unroll
+        for (int m = 0; m < NC; ++m) c[m] = -1.0f * ch[co + side * h + m * hs];
+#pragma unroll 1
+        for (int p = 0; p < L; ++p) {
+            const uint32_t* bp = w.beta + p * t.W;
+            double v[H];
+            const uint32_t* wq = bp + wb[V - 1] + side;
+#pragma unroll
+            for (int m = 0; m < H; ++m) v[m] = g_op((double)c[m], (double)c[m + H], (wq[2 * m] >> j) & 1u);
+            vside_levels<V - 2, FM>(v, bp, wb, j, side, gmask, t.lmax);  // levels V-2 .. 1 (level 0 below)
+#if PL_SCL_C7
+            if (w7) {
+                double* e = reinterpret_cast<double*>(&vc->v7[it * L + p]) + 2 * side;
+                e[0] = v[0];
+                e[1] = v[1];
+            }
+#endif
+            if ((gmask & 1u) != 0u) v[0] = g_op(v[0], v[1], ((bp + wb[0] + side)[0] >> j) & 1u);
+            else v[0] = f_op<FM>(v[0], v[1], t.lmax);
+            if (side == 0) {
+                xr[p] = v[0];
+            } else {
+                const double x = xr[p], y = v[0];
+                if (vc != nullptr) vc->v[it * L + p] = make_double2(x, y);  // the left pass (is_g false)
+                const double r = is_g ? g_op(x, y, getbit(bp, pos + j)) : f_op<FM>(x, y, t.lmax);
+                w.A[p * t.per + (1 << ls) - (1 << R) + j] = r;
+            }
+        }
+    }
+}
+
 // The right pass from the cache: per path, the owner's (x, y) and one g.  Every owner byte, cache
 // entry and partial-sum word of the pass is loaded before the first g, so the private-memory loads
 // (L2 latency) overlap instead of being paid once per path (r04n phase timing: 12.7k cycles per pass
@@ -840,6 +966,10 @@ __device__ void vvisit64(const St& t, int pos, bool is_g, int lane, const int* w
         const int c = idx >> ls, j = idx & (h - 1);
         const Cw w = t.cw(c);
         const int co = (int)(t.b0 + c < t.bs ? c : t.bs - 1 - t.b0) * t.n + j;
+        if constexpr (NS == 0 && CPW * 2 * L < 64) {  // X2: one side at a time (register budget)
+            vnode64_ns0<L, V, FM>(t, w, ch0, co, wb, j, gmask, is_g, pos, ls, vc, it, w7);
+            continue;
+        }
         float cx[NC], cy[NC];
 #pragma unroll
         for (int m = 0; m < NC; ++m) {
@@ -1144,6 +1274,8 @@ __device__ __forceinline__ void node_fg_st(const St& t, int pos, bool is_g, int 
 template <int L, int V, int FM, int CPW>
 __device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane, VCache<FM>* vc) {
     constexpr int LL = ilog2(L);
+    if constexpr (CPW * 2 * L < 64)  // X2: per-call lane addresses (not hoisted out of the decoder loop, where
+        asm volatile("" : "+v"(lane));  // they would hold VGPRs across the lane subtrees)
     const int ls = s - 1, h = 1 << ls;
     // the per-lane cache holds kVcEntries (item, path) entries.  Release builds run pick_v's V,
     // whose virtual nodes have h <= 32 (S = 10: V = 4; S = 9: V = 3; below: h = 16), i.e. at most
@@ -1800,6 +1932,134 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
     }
 }
 
+// The lane subtree with two rows per codeword (X2; L = 8, min-sum, no fast-SCL: the bench
+// kernel).  Row rr = (lane >> 4) & 1 of the codeword's row pair holds the elements j = 2 jl + rr
+// of the stage-3 (s3[jl], jl < 4), stage-2 (s2[jl], jl < 2) and stage-1 (s1) buffers; the f/g
+// between those stages pair elements j and j + 2^(s-1) (same parity), so they are row-local with
+// the local index jl.  The stage-1 node's two elements are exchanged between the rows (x0, x1)
+// and both rows compute the leaf value, the penalty, the rank (split between the rows) and the
+// selection; each row moves its own half of the live buffers.  Same operands, same operations and
+// same order as subtree(), so the same values.
+template <int L, int CPW>
+__device__ void subtree_x2(const St& t, int i0, uint32_t fz, double& pm, int& org, uint32_t& ps, int lane PROF_PARAM) {
+    static_assert(L == 8 && R == 4 && PL_SCL_PUSH == 1 && PL_SCL_PUSH_REFM && PL_SCL_FROZEN_PAIR,
+                  "X2: the L = 8 push-selection subtree");
+    constexpr int GW = 2 * L;
+    const int gl = lane & (GW - 1), gbase = lane & ~(GW - 1);
+    const bool hi = (gl & L) != 0;
+    const int rr = (lane >> 4) & 1;
+    const Cw w = t.cw(lane / (2 * GW));
+    const double lmax = t.lmax;
+    double s3[4], s2[2], s1 = 0.0, x0 = 0.0, x1 = 0.0;
+    ps = 0u;
+    org = gl & (L - 1);
+    const double* inA = w.A + org * t.per + rr;  // stage R at offset 0 of a path's region; this row's parity
+    bool pair = false;
+    (void)i0;
+#pragma unroll
+    for (int i = 0; i < T; ++i) {
+        if ((i & 1) && pair) continue;  // done with leaf i-1
+        if (i > 0) {  // nodes that ended at leaf i-1 (stages 1..ctz(i)): [uL ^ uR, uR]
+            const int tz = __builtin_ctz(i);
+            for (int s = 1; s <= tz; ++s) {
+                const int h = 1 << (s - 1), pos = i - (1 << s);
+                ps ^= (ps >> h) & (((1u << h) - 1u) << pos);
+            }
+            if (tz + 1 == R) inA = w.A + org * t.per + rr;  // the origin may have changed
+        }
+        // the leaf value l0 (leaf_llr): g at stage ctz(i)+1 into ctz(i), then f down
+        double l0;
+        {
+            const uint32_t psr = ps >> rr;  // bit p0 + 2 jl + rr of ps = bit p0 + 2 jl of psr
+            const int tz = i == 0 ? R : __builtin_ctz(i);
+            if (i == 0) {
+#pragma unroll
+                for (int jl = 0; jl < 4; ++jl) s3[jl] = f_ms(inA[2 * jl], inA[2 * jl + 8], lmax);
+            } else if (tz == 3) {
+#pragma unroll
+                for (int jl = 0; jl < 4; ++jl) s3[jl] = g_op(inA[2 * jl], inA[2 * jl + 8], (psr >> (2 * jl)) & 1u);
+            }
+            if (tz >= 3) {
+#pragma unroll
+                for (int jl = 0; jl < 2; ++jl) s2[jl] = f_ms(s3[jl], s3[jl + 2], lmax);
+            } else if (tz == 2) {
+                const int p0 = i - 4;
+#pragma unroll
+                for (int jl = 0; jl < 2; ++jl) s2[jl] = g_op(s3[jl], s3[jl + 2], (psr >> (p0 + 2 * jl)) & 1u);
+            }
+            if (tz >= 2) s1 = f_ms(s2[0], s2[1], lmax);
+            else if (tz == 1) s1 = g_op(s2[0], s2[1], (psr >> (i - 2)) & 1u);
+            if (tz >= 1) {
+                xch_rows(s1, x0, x1);
+                l0 = f_ms(x0, x1, lmax);
+            } else {
+                if (((fz >> (i - 1)) & 1u) == 0u) xch_rows(s1, x0, x1);  // leaf i-1 moved the state
+                l0 = g_op(x0, x1, (ps >> (i - 1)) & 1u);
+            }
+        }
+        PROF_MARK(8);
+        // frozen sibling pair: the shadow lanes take leaf i+1's value g(x0, x1, 0)
+        double lv = l0;
+        pair = (i & 1) == 0 && ((fz >> i) & 3u) == 3u;
+        if (pair && hi) lv = g_op(x0, x1, 0u);
+        const double l = fmax(fmin(lv, lmax), -lmax);
+        const bool info = ((fz >> i) & 1u) == 0u;
+        const double sl = (info && hi) ? -1.0 * l : 1.0 * l;
+        const double pen = pl::softplus_pm(-sl);
+        if (!info) {
+            if (pair) {
+                const double oth = half_xchg<L>(pen, lane);
+                pm = (pm + (hi ? oth : pen)) + (hi ? pen : oth);
+            } else {
+                pm = pm + pen;
+            }
+            PROF_MARK(9);
+            continue;
+        }
+#if PL_SCL_PROF
+        asm volatile("" ::"v"(pen));
+        PROF_MARK(9);
+#endif
+        const double cv = pm + pen;
+        const int dst = (gbase + rank16_x2(cv)) << 2;
+#if PL_SCL_PROF
+        asm volatile("" ::"v"(dst));
+        PROF_MARK(10);
+#endif
+        pm = push_d<L>(cv, dst);
+        ps = (uint32_t)push_i<L>((int)(ps | ((hi ? 1u : 0u) << i)), dst);
+        org = push_i<L>(org, dst);
+        inA = w.A + org * t.per + rr;
+        // the live buffers (left half of their node at leaf i): stage 3 moved; stage 2 / 1 the f of
+        // the moved parent when that is live too, else moved (push_live)
+        if (((i >> 2) & 1) == 0) {
+#pragma unroll
+            for (int jl = 0; jl < 4; ++jl) s3[jl] = push_d<L>(s3[jl], dst);
+        }
+        if (((i >> 1) & 1) == 0) {
+            if (((i >> 2) & 1) == 0) {
+#pragma unroll
+                for (int jl = 0; jl < 2; ++jl) s2[jl] = f_ms(s3[jl], s3[jl + 2], lmax);
+            } else {
+#pragma unroll
+                for (int jl = 0; jl < 2; ++jl) s2[jl] = push_d<L>(s2[jl], dst);
+            }
+        }
+        if ((i & 1) == 0) {
+            if (((i >> 1) & 1) == 0) s1 = f_ms(s2[0], s2[1], lmax);
+            else s1 = push_d<L>(s1, dst);
+        }
+#if PL_SCL_PROF
+        asm volatile("" ::"v"(pm), "v"(ps), "v"(org));
+        PROF_MARK(11);
+#endif
+    }
+    for (int s = 1; s <= R; ++s) {  // the nodes ending at the last leaf, up to stage R
+        const int h = 1 << (s - 1), pos = T - (1 << s);
+        ps ^= (ps >> h) & (((1u << h) - 1u) << pos);
+    }
+}
+
 // Metric term of element j of a virtual stage-s node (D = S - s stages below the channel).
 template <int D, int FM>
 __device__ __noinline__ double vterm(const float* ch, const uint32_t* bp, int s, int pos, int j, double sg,
@@ -1872,28 +2132,31 @@ __device__ void repoint(const St& t, int i0, int lane) {
     constexpr int LL = ilog2(L);
 #if PL_SCL_REPOINT_VEC
     if (V >= 2 || t.W >= 4) {  // V >= 2: n >= 128, so W >= 4 (the word loop below is not compiled in)
-        // two lanes per (codeword, path) pair (CPW * L = 32): one origin load each, the pair's
-        // partial-sum row in 16-byte quads (words past i0 are copied too: they belong to leaves
-        // not decided yet and are overwritten before anything reads them) and its 16-byte
-        // stage-owner row -- 6 LDS loads and 5 stores per lane instead of 22 and 22
+        // LPP = 64 / (CPW * L) lanes per (codeword, path) pair (2 at CPW * L = 32, 4 with two rows
+        // per codeword): one origin load each, the pair's partial-sum row in 16-byte quads (words
+        // past i0 are copied too: they belong to leaves not decided yet and are overwritten before
+        // anything reads them) and its 16-byte stage-owner row -- 6 LDS loads and 5 stores per
+        // lane instead of 22 and 22 (LPP = 2)
+        constexpr int LPP = 64 / (CPW * L), QPL = 8 / LPP;  // quads per lane (W <= 32 words = 8 quads)
+        static_assert(64 % (CPW * L) == 0 && LPP >= 2 && LPP <= 8, "repoint: lanes per (codeword, path) pair");
         asm volatile("" : "+v"(lane));  // per-call addresses (not hoisted out of the decoder loop)
-        const int cp = lane >> 1, h = lane & 1, p = cp & (L - 1);
+        const int cp = lane >> ilog2(LPP), h = lane & (LPP - 1), p = cp & (L - 1);  // lane is opaque: shifts, not signed division
         const Cw cw = t.cw(cp >> LL);
         const int o = cw.org_s[p];
         const int nq = min(t.W >> 2, (((i0 + 31) >> 5) + 3) >> 2);
         const uint4* src = reinterpret_cast<const uint4*>(cw.beta + o * t.W);
-        uint4 v0 = make_uint4(0u, 0u, 0u, 0u), v1 = v0, v2 = v0, v3 = v0, sp = v0;
+        uint4 v0 = make_uint4(0u, 0u, 0u, 0u), v1 = v0, v2 = v0, v3 = v0, sp = v0;  // QPL <= 4 quads
         if (h < nq) v0 = src[h];
-        if (h + 2 < nq) v1 = src[h + 2];
-        if (h + 4 < nq) v2 = src[h + 4];
-        if (h + 6 < nq) v3 = src[h + 6];
+        if (QPL > 1 && h + LPP < nq) v1 = src[h + LPP];
+        if (QPL > 2 && h + 2 * LPP < nq) v2 = src[h + 2 * LPP];
+        if (QPL > 3 && h + 3 * LPP < nq) v3 = src[h + 3 * LPP];
         if (h == 0) sp = *reinterpret_cast<const uint4*>(cw.sptr + o * SPS);
         __syncthreads();
         uint4* dst = reinterpret_cast<uint4*>(cw.beta + p * t.W);
         if (h < nq) dst[h] = v0;
-        if (h + 2 < nq) dst[h + 2] = v1;
-        if (h + 4 < nq) dst[h + 4] = v2;
-        if (h + 6 < nq) dst[h + 6] = v3;
+        if (QPL > 1 && h + LPP < nq) dst[h + LPP] = v1;
+        if (QPL > 2 && h + 2 * LPP < nq) dst[h + 2 * LPP] = v2;
+        if (QPL > 3 && h + 3 * LPP < nq) dst[h + 3 * LPP] = v3;
         if (h == 0) *reinterpret_cast<uint4*>(cw.sptr + p * SPS) = sp;
         __syncthreads();
         return;
@@ -1977,7 +2240,7 @@ __device__ void upper_prune(const St& t, int s, int pos, int kind, double& pm, i
 template <int L, int V, int FM, bool FAST>
 __global__ __launch_bounds__(64)
 #if PL_SCL_WPE > 0
-__attribute__((amdgpu_waves_per_eu(PL_SCL_WPE)))
+__attribute__((amdgpu_waves_per_eu(xrep<L, V, FM, FAST>() == 2 ? PL_SCL_X2_WPE : PL_SCL_WPE)))
 #endif
 void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict__ out,
                                                       int out_kind, double* __restrict__ out_pm,
@@ -1985,7 +2248,8 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
                                                       const int32_t* __restrict__ info_pos, int n, int S, int k,
                                                       double lmax, int crc_deg, uint32_t crc_g,
                                                       double* __restrict__ vcache) {
-    constexpr int GW = 2 * L, CPW = 64 / GW, LL = ilog2(L);
+    constexpr int X = xrep<L, V, FM, FAST>();  // rows per codeword (X2: 2)
+    constexpr int GW = 2 * L, CPW = 64 / (GW * X), LL = ilog2(L);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x;
     St t;
@@ -2002,7 +2266,8 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
     t.lmax = lmax;
     t.vcache = (FM == 1 && V >= 1 && vcache != nullptr) ? vcache + t.b0 * cache_size(n, V) : nullptr;
     const int W = t.W, LW = ilog2(W);
-    const int gl = lane & (GW - 1), my_c = lane / GW;
+    const int gl = lane & (GW - 1), my_c = lane / (GW * X);
+    const bool own = X == 1 || ((lane / GW) & (X - 1)) == 0;  // the codeword's first row writes its per-path LDS state
     const Cw mine = t.cw(my_c);
     pl::sp_load_tables(lane, 64);  // the penalty's log table (softplus.h, PL_SP_FORM 3)
     PROF_DECL;
@@ -2141,15 +2406,19 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
         } else {
             int org;
             uint32_t ps;
-            subtree<L, FM, CPW, FAST>(t, i0, frozen_words[i0 >> 5] >> (i0 & 31), pm, org, ps, lane PROF_ARG);
+            if constexpr (X == 2) {
+                subtree_x2<L, CPW>(t, i0, frozen_words[i0 >> 5] >> (i0 & 31), pm, org, ps, lane PROF_ARG);
+            } else {
+                subtree<L, FM, CPW, FAST>(t, i0, frozen_words[i0 >> 5] >> (i0 & 31), pm, org, ps, lane PROF_ARG);
+            }
             PROF_MARK(2);
             // re-point the upper-tree state of every path to its origin's, then store the
             // subtree's partial sums: partial-sum words before i0 and stage owners R..SS
-            if (gl < L) mine.org_s[gl] = org;
+            if (gl < L && own) mine.org_s[gl] = org;
             __syncthreads();
             if (!PL_SCL_DIAG_NO_REPOINT) repoint<L, V, CPW>(t, i0, lane);
             const int w_i = i0 >> 5, off = i0 & 31;
-            if (gl < L) {
+            if (gl < L && own) {
                 uint32_t* bw = mine.beta + gl * W + w_i;
                 *bw = off == 0 ? ps : ((*bw & ((1u << off) - 1u)) | (ps << off));
             }
@@ -2164,7 +2433,7 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
             for (int s = R + 1; s <= top2; ++s) combine_upper<L, CPW>(t, s, nxt - (1 << s), lane);
         PROF_MARK(4);
     }
-    if (gl < L) mine.pm_s[gl] = pm;
+    if (gl < L && own) mine.pm_s[gl] = pm;
 
     // u = x G_n per path (x = the root's partial sums): in-word spans, then word spans
     for (int idx = lane; idx < CPW * L * W; idx += 64) {
@@ -2189,7 +2458,7 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
     }
 
     // CRC check per path (my_sn dec.py:507-518)
-    if (gl < L) {
+    if (gl < L && own) {
         int f = 0;
         if (crc_deg > 0) {
             const uint32_t* U = mine.beta + gl * W;
@@ -2218,12 +2487,14 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
             rk += (v < mv || (v == mv && c < gl)) ? 1 : 0;
         }
         const double val = mv + (mine.fail_s[p] ? t.lmax * (double)k : 0.0);
-        mine.sv[rk] = val;
-        mine.sp[rk] = p;
-        if (out_pm != nullptr && t.b0 + my_c < bs) out_pm[(t.b0 + my_c) * GW + rk] = val;
+        if (own) {
+            mine.sv[rk] = val;
+            mine.sp[rk] = p;
+            if (out_pm != nullptr && t.b0 + my_c < bs) out_pm[(t.b0 + my_c) * GW + rk] = val;
+        }
     }
     __syncthreads();
-    if (gl == 0) {
+    if (gl == 0 && own) {
         double bestv = mine.sv[0];
         int best = mine.sp[0];
         for (int r = 1; r < GW; ++r)
@@ -2358,7 +2629,9 @@ int launch_scl_tree(const pl_plan* p, const float* llr, int64_t bs, void* out, i
     }
 #endif
     const Lay y = make_layout(p->n, S, L, V);
-    const int cpw = 32 / L;  // codewords per wave (one 2L-lane group each)
+    // codewords per wave: one 2L-lane group each, or two rows each (X2: the L = 8 min-sum kernel at V = 4)
+    const int X = (L == 8 && V == 4) ? (exact ? xrep<8, 4, 1, false>() : fast ? xrep<8, 4, 0, true>() : xrep<8, 4, 0, false>()) : 1;
+    const int cpw = 32 / L / X;
     const int lds = cpw * y.bytes;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
