@@ -228,14 +228,15 @@ def _time_launches(fn, steps, warmup, settle_ms, dev):
     return e0.elapsed_time(e1) / steps
 
 
-def config_line(decoder, k, n, bs, L, ebno, dev, rank, steps, warmup):
+def config_line(decoder, k, n, bs, L, ebno, dev, rank, steps, warmup, fmode=0):
     """One more BASELINE.json configuration on this GPU, measured after the headline's timed
     region: kernel ms per launch (HIP events over back-to-back launches on one resident batch),
-    Mcodewords/s, info Gbit/s, BLER, and the HBM roofline of the launch (bs (4n + 4k) bytes)."""
+    Mcodewords/s, info Gbit/s, BLER, and the HBM roofline of the launch (bs (4n + 4k) bytes).
+    fmode 1: the exact boxplus f (my_sn SC_Dec / SCL_Dec)."""
     import polar_amd
     from polar_amd import _lib, channel, ops
     fp = polar_amd.reference_frozen_pos(k, n)
-    plan = _lib.Plan(n, polar_amd.frozen_mask(fp, n), L, _lib.PL_F_MINSUM, device=dev)
+    plan = _lib.Plan(n, polar_amd.frozen_mask(fp, n), L, fmode, device=dev)
     gen = torch.Generator(device=dev).manual_seed(1042 + rank)
     model = channel.System_AWGN_model(n, k, channel.GpuEncoder(fp, n), None, device=dev, generator=gen)
     with torch.no_grad():
@@ -251,13 +252,47 @@ def config_line(decoder, k, n, bs, L, ebno, dev, rank, steps, warmup):
     nerr = int(torch.any(out != bits, dim=-1).sum().item())
     nbytes = bs * (4 * n + 4 * k)
     ach = nbytes / (ms * 1e-3) / 1e9
-    res = {"workload": f"{'SCL' if L > 1 else 'SC'} decode (k={k}, n={n}), bs={bs}" + (f", L={L}" if L > 1 else ""),
+    res = {"workload": f"{'SCL' if L > 1 else 'SC'} decode (k={k}, n={n}), bs={bs}" + (f", L={L}" if L > 1 else "")
+           + (", exact boxplus f (my_sn)" if fmode == 1 else ""),
            "kernel": plan.kernel()[0], "kernel_ms": round(ms, 5), "steps": steps,
            "mcw_s": round(bs / ms / 1e3, 3), "info_gbit_s": round(bs * k / ms / 1e6, 4),
            "dtype": "f64" if L > 1 else "f32", "bler": round(nerr / bs, 6),
            "roofline_hbm": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": round(ach / HBM_PEAK_GBS, 5), "algorithmic_bytes_per_launch": nbytes}}
     return res, fn, plan, llr, out
+
+
+def library_src_hash():
+    """The source hash the loaded libpolar_mi355x.so was built from (pl_version)."""
+    from polar_amd import _lib
+    return _lib.lib().pl_version().decode().split()[-1]
+
+
+def latency_bound(tag, kern_ms):
+    """Independent critical-path bound of a batch that fills less than one wave per SIMD
+    (profiles/latency.json, tools/isa_walk.py chain): the longest register-dependence chain of one
+    wave's instruction stream, each edge weighted by the single-wave dependent latency
+    tools/micro/chain_latency.hip measured for its form, plus the back-to-back launch floor of an
+    empty kernel with the same grid.  frac = bound / measured kernel time (1.0: the launch costs no
+    more than its dependent chain).  Also the in-order single-wave estimate (issue in program
+    order after the sources are ready).  null when the record was made from other sources."""
+    path = os.path.join(ROOT, "profiles", "latency.json")
+    try:
+        rec = json.load(open(path))[tag]
+    except Exception:
+        return None
+    out = {"bound": "latency", "source": "profiles/latency.json", "chain_cycles": rec["chain_cycles"],
+           "clock_ghz": rec["clock_ghz"], "latency_table": rec["latency_table"]}
+    if rec.get("src_hash") != library_src_hash() or not rec.get("clock_ghz"):
+        out.update({"stale": True, "frac": None})
+        return out
+    floor = rec["launch_floor_us"].get("256")
+    bound_ms = (rec["chain_us"] + floor) / 1e3
+    est_ms = (rec["in_order_us"] + floor) / 1e3
+    out.update({"stale": False, "launch_floor_us": floor, "chain_us": rec["chain_us"], "bound_ms": round(bound_ms, 5),
+                "in_order_estimate_ms": round(est_ms, 5), "achieved_ms": round(kern_ms, 5),
+                "frac": round(bound_ms / kern_ms, 4), "frac_in_order": round(est_ms / kern_ms, 4)})
+    return out
 
 
 def latency_roofline(plan, llr, k, n, bs, ms_full, dev, steps=400):
@@ -315,6 +350,27 @@ def valu_roofline(tag, kern_ms):
     on gfx950 (SQ_ACTIVE_INST_VALU / SQ_THREAD_CYCLES_VALU count instructions), so none is reported.
     null fields when the profile was taken on another instruction stream than the built kernel's."""
     v = valu_from_profiles(tag)
+    if v and "static" in v:
+        st = v["static"]
+        fresh = st.get("isa_sha") == current_isa_sha(tag) if current_isa_sha(tag) else st.get("src_hash") == library_src_hash()
+        out = {"bound": "valu_issue", "unit": "us of VALU issue per SIMD per launch", "kernel_ms": round(kern_ms, 5),
+               "method": "per-mnemonic: the walked instruction stream (tools/isa_walk.py) x calibrated issue cost per "
+                         "form (tools/micro/valu_cycles.hip); the residual against SQ_INSTS_VALU as a cost range",
+               "valu_per_wave_walk": st["valu_per_wave_walk"], "valu_per_wave_sq": st["valu_per_wave_sq"],
+               "calibration": st["calibration"], "stale": not fresh}
+        if not fresh:
+            out.update({"frac": None, "frac_lo": None, "frac_hi": None})
+            return out
+        waves = v.get("waves_per_launch") or st.get("waves_per_launch")
+        ns = st["issue_ns_per_wave"]
+        simd_ns = kern_ms * 1e6 * 1024
+        lo = (ns["mapped"] + ns["rest_lo"]) * waves / simd_ns
+        hi = (ns["mapped"] + ns["rest_hi"]) * waves / simd_ns
+        out.update({"frac": round((lo + hi) / 2, 4), "frac_lo": round(lo, 4), "frac_hi": round(hi, 4),
+                    "achieved": round((lo + hi) / 2 * kern_ms * 1e3, 2), "peak": round(kern_ms * 1e3, 2),
+                    "wait_share_per_wave": round(v["per_wave"]["WAIT_ANY"] / v["per_wave"]["WAVE_CYCLES"], 4)
+                    if "per_wave" in v and "WAIT_ANY" in v["per_wave"] else None})
+        return out
     if not v or "issue_ns_simd_per_launch" not in v:
         return None
     out = {"bound": "valu_issue", "unit": "us of VALU issue per SIMD per launch", "kernel_ms": round(kern_ms, 5),
@@ -449,12 +505,18 @@ def main():
         # BASELINE.json configs[1] (k=128, n=256, bs=4096, SC) and configs[3] (k=512, n=1024,
         # L=8, bs=8192, SCL) on this GPU, after the headline's timed region
         c1, _, p1, l1, _ = config_line("sc", 128, 256, 4096, 1, a.ebno, dev, rank, 2000, 200)
-        c1["roofline_latency"] = latency_roofline(p1, l1, 128, 256, 4096, c1["kernel_ms"], dev)
+        c1["roofline_latency"] = latency_bound("sc_k128_n256", c1["kernel_ms"])
+        c1["single_wave"] = latency_roofline(p1, l1, 128, 256, 4096, c1["kernel_ms"], dev)
         c3, _, _, _, _ = config_line("scl", 512, 1024, 8192, 8, a.ebno, dev, rank, 20, 3)
         rv = valu_roofline("scl_k512_n1024_bs8192_L8", c3["kernel_ms"])
         if rv is not None:
             c3["roofline_valu"] = rv
-        configs = {"configs_1": c1, "configs_3": c3}
+        # my_sn SC_Dec (the library API's default decoder, exact boxplus f) at the headline shape
+        cx, _, _, _, _ = config_line("sc", 512, 1024, 65536, 1, a.ebno, dev, rank, 50, 10, fmode=1)
+        rv = valu_roofline("sc_exact_k512_n1024_bs65536", cx["kernel_ms"])
+        if rv is not None:
+            cx["roofline_valu"] = rv
+        configs = {"configs_1": c1, "configs_3": c3, "mysn_sc_exact": cx}
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(llr.cpu().numpy(), fp.numpy(), k, n, a.decoder, L, a.cpu_seconds)

@@ -583,12 +583,39 @@ __device__ __forceinline__ float f_exact_wide(float x, float y, float lmax) {
 // exp_cr's range |x| <= 87 holds for every argument f forms when llr_max <= 43 (|xc + yc| <= 86)
 constexpr float kExactFastLmax = 43.0f;
 
+// clip(x, +-lmax) (dec.py:39-40) as one v_med3_f32 instead of the canonicalising v_max / v_min
+// pairs fminf(fmaxf(x, -lmax), lmax) compiles to (LLRs are never NaN: DESIGN.md section 7); the
+// same value for every other input, +-0 included
+#ifndef PL_EXF_MED3
+#define PL_EXF_MED3 1
+#endif
+__device__ __forceinline__ float clip_l(float x, float lmax) {
+#if PL_EXF_MED3
+    return __builtin_amdgcn_fmed3f(x, -lmax, lmax);
+#else
+    return fminf(fmaxf(x, -lmax), lmax);
+#endif
+}
+// the plan's llr_max is the same in every lane: taken as a scalar, the wide-range test is a scalar
+// branch instead of an exec-mask if/else (the out-of-line f receives it in a VGPR)
+#ifndef PL_EXF_UNIFORM
+#define PL_EXF_UNIFORM 1
+#endif
+__device__ __forceinline__ float uniform_l(float lmax) {
+#if PL_EXF_UNIFORM
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, lmax)));
+#else
+    return lmax;
+#endif
+}
+
 // f of my_sn/fec/polar/dec.py:39-43 on clipped inputs, each operation rounded as the reference does.
 // Out of line: inlined into the fully unrolled specialised SC kernels (hundreds of f per lane) the
 // fp64 code made one (128,256) kernel take minutes to compile.
 __device__ __attribute__((noinline)) float f_exact(float x, float y, float lmax) {
+    lmax = uniform_l(lmax);
     if (lmax > kExactFastLmax) return f_exact_wide(x, y, lmax);
-    const float xc = fminf(fmaxf(x, -lmax), lmax), yc = fminf(fmaxf(y, -lmax), lmax);
+    const float xc = clip_l(x, lmax), yc = clip_l(y, lmax);
 #if PL_EXF_LEAN
     const double ex = exp_d(xc), ey = exp_d(yc);
     float o = log_cr(1.0f + exp_sum(ex, ey, xc, yc));
@@ -607,9 +634,10 @@ struct f2 {
     float a, b;
 };
 __device__ __attribute__((noinline)) f2 f_exact2(float x0, float y0, float x1, float y1, float lmax) {
+    lmax = uniform_l(lmax);
     if (lmax > kExactFastLmax) return f2{f_exact_wide(x0, y0, lmax), f_exact_wide(x1, y1, lmax)};
-    const float xc0 = fminf(fmaxf(x0, -lmax), lmax), yc0 = fminf(fmaxf(y0, -lmax), lmax);
-    const float xc1 = fminf(fmaxf(x1, -lmax), lmax), yc1 = fminf(fmaxf(y1, -lmax), lmax);
+    const float xc0 = clip_l(x0, lmax), yc0 = clip_l(y0, lmax);
+    const float xc1 = clip_l(x1, lmax), yc1 = clip_l(y1, lmax);
 #if PL_EXF_LEAN
     const double ea0 = exp_d(xc0), ea1 = exp_d(xc1), eb0 = exp_d(yc0), eb1 = exp_d(yc1);
     const float s0 = exp_sum(ea0, eb0, xc0, yc0), s1 = exp_sum(ea1, eb1, xc1, yc1);

@@ -368,8 +368,9 @@ __device__ uint32_t lnode(float a, const Lane& ln);
 // 1 exp + 1 log per lane (S < G) or 2 + 1 (S = G) instead of 3 + 2.
 template <int S, bool TOP>
 __device__ __attribute__((noinline)) float f_lane_exact(float a, float y, uint32_t role31, float lmax) {
+    lmax = plx::uniform_l(lmax);
     if (lmax > plx::kExactFastLmax) return plx::f_exact_wide(a, y, lmax);
-    const float xc = fminf(fmaxf(a, -lmax), lmax), yc = fminf(fmaxf(y, -lmax), lmax);
+    const float xc = plx::clip_l(a, lmax), yc = plx::clip_l(y, lmax);
     const bool A = (int32_t)role31 < 0;
     float arg;
     if constexpr (TOP) {

@@ -62,9 +62,11 @@ def parse(asm, kernel="pl_sc_static_f32"):
 def walk(ins):
     """The common path: rare-case tests skipped (s_cbranch_vccz taken, s_cbranch_vccnz not taken:
     the zero/tie fix-ups and the missing-row stores are guarded that way), the vector output path
-    taken (s_cbranch_scc1), loops left at their exit.  Returns the instruction indices in order."""
+    taken (s_cbranch_scc1), loops left at their exit; in the exact-f functions the lane-divergent
+    llr_max test's fast arm entered (s_cbranch_execnz after the s_xor_b64 of a saveexec) and its
+    empty else arm skipped (after s_andn2_saveexec_b64).  Returns the instruction indices in order."""
     lab = {t: i for i, (k, t) in enumerate(ins) if k == "label"}
-    pc, trace = 0, []
+    pc, trace, prev, cmp43 = 0, [], "", False
     while pc < len(ins) and len(trace) < 10 ** 6:
         k, t = ins[pc]
         if k == "label":
@@ -72,19 +74,59 @@ def walk(ins):
             continue
         m = t.split()[0]
         trace.append(pc)
-        if m == "s_endpgm":
+        if m.startswith("v_cmp"):  # the exact f's range test: llr_max against 43.0 (0x422c0000)
+            cmp43 = m.startswith("v_cmp_ngt_f32") and any(
+                ins[j][0] == "ins" and "0x422c0000" in ins[j][1] for j in range(max(0, pc - 6), pc))
+        if m in ("s_endpgm", "s_setpc_b64"):
             break
         if m == "s_branch":
             pc = lab[t.split()[1]]
+            prev = m
             continue
         if m.startswith("s_cbranch"):
             tgt = lab[t.split()[1]]
-            take = {"s_cbranch_scc1": True, "s_cbranch_execz": False, "s_cbranch_vccz": True,
-                    "s_cbranch_vccnz": False}.get(m, tgt > pc)  # execnz: backward = loop (exit)
+            if m in ("s_cbranch_vccz", "s_cbranch_vccnz") and cmp43:
+                take = m == "s_cbranch_vccnz"  # the llr_max <= 43 test (exactf.h): true in every lane
+            elif m == "s_cbranch_execnz":
+                take = prev == "s_xor_b64" and tgt > pc
+            elif m == "s_cbranch_execz":
+                take = prev == "s_andn2_saveexec_b64"
+            else:
+                take = {"s_cbranch_scc1": True, "s_cbranch_execz": False, "s_cbranch_vccz": True,
+                        "s_cbranch_vccnz": False}.get(m, tgt > pc)
             pc = tgt if take else pc + 1
+            prev = m
             continue
+        prev = m
         pc += 1
     return trace
+
+
+def callees(ins, trace):
+    """Counter of the functions the walked stream calls (s_swappc_b64 through a register pair set by
+    s_getpc_b64 + s_add_u32 SYM@rel32@lo)."""
+    pair, calls = {}, Counter()
+    for i in trace:
+        t = ins[i][1]
+        mm = re.match(r"s_add_u32 s(\d+), s\d+, (\S+)@rel32@lo", t)
+        if mm:
+            pair[int(mm.group(1))] = mm.group(2)
+        mm = re.match(r"s_swappc_b64 s\[30:31\], s\[(\d+):\d+\]", t)
+        if mm:
+            calls[pair.get(int(mm.group(1)), "?")] += 1
+    return calls
+
+
+def dynamic_histogram(asm, kernel):
+    """Histogram of the walked kernel stream plus, per call, the walked stream of its callee."""
+    ins = parse(asm, kernel)
+    tr = walk(ins)
+    h = histogram(ins, tr)
+    for fn, c in callees(ins, tr).items():
+        fi = parse(asm, fn)
+        for m, v in histogram(fi, walk(fi)).items():
+            h[m] += v * c
+    return h, ins, tr
 
 
 def unit(m):
@@ -305,6 +347,79 @@ def chain(ins, trace, lat):
     return longest, end
 
 
+def isa_sha(asm, kernel="pl_sc_static_f32"):
+    """The instruction-stream hash tests/golden/kernel_isa.json pins (test_kernel_resources.isa_summary)."""
+    import test_kernel_resources as t
+    return t.isa_summary(asm, lambda nm: nm == kernel)[kernel]["sha"]
+
+
+def record_valu(asm, tag, cal_path, sq_valu_per_wave=None, waves_per_launch=None, codewords_per_wave=None):
+    """profiles/valu.json[tag]["static"]: the walked stream's VALU per wave by mnemonic, each with
+    its calibrated issue cost (tools/micro/valu_cycles.hip), and the residual against the SQ
+    counter (instructions the walk does not see: rare fallbacks) carried as a cost range."""
+    cal = calibration(cal_path)
+    h, ins, tr = dynamic_histogram(asm, "pl_sc_static_f32")
+    by = {}
+    mapped_ns, unmapped = 0.0, Counter()
+    for m, c in sorted(h.items(), key=lambda x: -x[1]):
+        if unit(m) != "valu":
+            continue
+        b = base_mnemonic(m)
+        form = CAL_MAP.get(b)
+        cost = cal.get(form) if form else None
+        by[m] = [c, form, cost]
+        if cost is None:
+            unmapped[m] += c
+        else:
+            mapped_ns += c * cost
+    walk_valu = sum(c for m, c in h.items() if unit(m) == "valu")
+    lo_c = min(v for k, v in cal.items() if k != "v_exp_f32")
+    hi_c = max(v for k, v in cal.items() if k != "v_exp_f32")
+    resid = (sq_valu_per_wave - walk_valu) if sq_valu_per_wave is not None else 0.0
+    un = sum(unmapped.values())
+    from polar_amd import build as _b
+    rec = {"isa_sha": isa_sha(asm), "src_hash": _b.source_hash(), "calibration": cal_path, "valu_per_wave_walk": walk_valu,
+           "valu_per_wave_sq": sq_valu_per_wave, "residual_per_wave": round(resid, 1),
+           "issue_ns_per_wave": {"mapped": round(mapped_ns, 1),
+                                 "rest_lo": round((un + max(resid, 0)) * lo_c, 1),
+                                 "rest_hi": round((un + max(resid, 0)) * hi_c, 1)},
+           "unmapped": dict(unmapped), "by_mnemonic": by,
+           "units_per_wave": dict(Counter({unit(m): 0 for m in h}) + Counter({u: sum(c for m, c in h.items() if unit(m) == u) for u in ("valu", "salu", "lds", "vmem", "smem")})),
+           "calls_per_wave": dict(callees(ins, tr)), "waves_per_launch": waves_per_launch,
+           "codewords_per_wave": codewords_per_wave}
+    path = os.path.join(ROOT, "profiles", "valu.json")
+    vj = json.load(open(path)) if os.path.exists(path) else {}
+    vj.setdefault(tag, {})["static"] = rec
+    json.dump(vj, open(path, "w"), indent=1)
+    return rec
+
+
+def record_chain(asm, tag, lat_path, kernel_ms=None):
+    """profiles/latency.json[tag]: the walked stream's longest register-dependence chain (cycles,
+    chain_latency.hip's per-form latencies) and the in-order single-wave estimate, in us at the
+    measured s_memtime clock, plus the back-to-back launch floor."""
+    lat = latency_table(lat_path)
+    clock = None
+    for line in open(lat_path):
+        mm = re.match(r"^s_memtime clock: ([\d.]+) GHz", line)
+        if mm:
+            clock = float(mm.group(1))
+    ins = parse(asm)
+    tr = walk(ins)
+    longest, est = chain(ins, tr, lat)
+    from polar_amd import build as _b
+    rec = {"isa_sha": isa_sha(asm), "src_hash": _b.source_hash(), "latency_table": lat_path, "instructions_per_wave": len(tr),
+           "chain_cycles": round(longest, 1), "in_order_cycles": round(est, 1), "clock_ghz": clock,
+           "chain_us": round(longest / clock / 1e3, 3) if clock else None,
+           "in_order_us": round(est / clock / 1e3, 3) if clock else None,
+           "launch_floor_us": {k[7:]: v for k, v in lat.items() if k.startswith("launch_")}}
+    path = os.path.join(ROOT, "profiles", "latency.json")
+    lj = json.load(open(path)) if os.path.exists(path) else {}
+    lj[tag] = rec
+    json.dump(lj, open(path, "w"), indent=1)
+    return rec
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("cmd", choices=["hist", "valu", "chain"])
@@ -313,8 +428,12 @@ def main():
     ap.add_argument("--cal", default=None)
     ap.add_argument("--lat", default=None)
     ap.add_argument("--asm", default=None, help="read the assembly from this file instead of compiling")
+    ap.add_argument("--fm", type=int, default=0, help="f mode of the plan (1: the exact boxplus f)")
+    ap.add_argument("--tag", default=None, help="valu.json / latency.json key")
+    ap.add_argument("--bs", type=int, default=65536)
+    ap.add_argument("--cpw", type=int, default=None, help="codewords per wave (64 / lanes per codeword)")
     a = ap.parse_args()
-    asm = open(a.asm).read() if a.asm else kernel_asm(a.k, a.n)
+    asm = open(a.asm).read() if a.asm else kernel_asm(a.k, a.n, a.fm)
     ins = parse(asm)
     trace = walk(ins)
     hist = histogram(ins, trace)
@@ -327,16 +446,15 @@ def main():
             print(f"{m:28s} {c}")
         return
     if a.cmd == "valu":
-        cal = calibration(a.cal)
-        ns, unmapped, lo_c, hi_c = valu_issue(hist, cal)
-        print(json.dumps({"valu_per_wave_walk": units["valu"], "issue_ns_per_wave_mapped": round(ns, 1),
-                          "unmapped": dict(unmapped), "unmapped_cost_range_ns": [lo_c, hi_c]}))
+        tag = a.tag or f"sc_k{a.k}_n{a.n}_bs{a.bs}"
+        vj = json.load(open(os.path.join(ROOT, "profiles", "valu.json")))
+        sq = vj.get(tag, {}).get("per_wave", {}).get("INSTS_VALU")
+        rec = record_valu(asm, tag, a.cal, sq, vj.get(tag, {}).get("waves_per_launch"), a.cpw)
+        print(json.dumps({k: rec[k] for k in ("valu_per_wave_walk", "valu_per_wave_sq", "issue_ns_per_wave", "unmapped")}))
         return
     if a.cmd == "chain":
-        lat = latency_table(a.lat)
-        longest, est = chain(ins, trace, lat)
-        print(json.dumps({"instructions": len(trace), "chain_cycles": round(longest, 1),
-                          "in_order_cycles": round(est, 1), "launch_floor_us": {k: v for k, v in lat.items() if k.startswith("launch")}}))
+        rec = record_chain(asm, a.tag or f"sc_k{a.k}_n{a.n}", a.lat)
+        print(json.dumps({k: v for k, v in rec.items() if k != "latency_table"}))
 
 
 if __name__ == "__main__":

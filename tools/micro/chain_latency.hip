@@ -68,6 +68,19 @@ __global__ __launch_bounds__(64) void c_gload(float* out, float a, unsigned long
     if (threadIdx.x == 0) *tm = t1 - t0;
 }
 
+// s_memtime and s_memrealtime across one long dependent chain of one wave
+__global__ __launch_bounds__(64) void c_clock(float* out, float a, unsigned long long* tm) {
+    float x = threadIdx.x * 0.001f;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    for (int it = 0; it < 64 * ITER; ++it) asm volatile("v_add_f32 %0, %0, %1" : "+v"(x) : "v"(a));
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    out[threadIdx.x] = x;
+    if (threadIdx.x == 0) {
+        tm[0] = t1 - t0;
+        tm[1] = r1 - r0;
+    }
+}
+
 typedef void (*Kern)(float*, float, unsigned long long*);
 
 int main() {
@@ -128,16 +141,15 @@ int main() {
         (void)hipEventElapsedTime(&t, e0, e1);
         printf("empty kernel, %4d blocks   %.3f us per back-to-back launch\n", blocks, t * 1e3 / N);
     }
-    // the s_memtime clock: cycles of a 1024-block v_add_f32 launch against its event time
+    // the s_memtime clock against s_memrealtime (100 MHz): one long single-wave chain, clock up
     {
-        hipLaunchKernelGGL(c_add_f32, dim3(1), dim3(64), 0, 0, buf, 1.0001f, tmd);
-        (void)hipEventRecord(e0);
-        hipLaunchKernelGGL(c_add_f32, dim3(1), dim3(64), 0, 0, buf, 1.0001f, tmd);
-        (void)hipEventRecord(e1);
-        (void)hipEventSynchronize(e1);
-        unsigned long long c = 0;
-        (void)hipMemcpy(&c, tmd, 8, hipMemcpyDeviceToHost);
-        printf("s_memtime: %llu cycles for the v_add_f32 chain of one wave\n", c);
+        hipLaunchKernelGGL(c_add_f32, dim3(1024), dim3(64), 0, 0, buf, 1.0001f, tmd + 1);
+        hipLaunchKernelGGL(c_clock, dim3(1), dim3(64), 0, 0, buf, 1.0001f, tmd);
+        (void)hipDeviceSynchronize();
+        unsigned long long c[2] = {0, 0};
+        (void)hipMemcpy(c, tmd, 16, hipMemcpyDeviceToHost);
+        printf("s_memtime clock: %.4f GHz (%llu cycles in %llu ticks of s_memrealtime at 100 MHz)\n",
+               (double)c[0] / ((double)c[1] * 10.0), c[0], c[1]);
     }
     (void)hipFree(buf);
     return 0;
