@@ -177,11 +177,16 @@ std::string static_source(int n, const uint8_t* frozen, int f_mode) {
     std::ostringstream o;
     o << "// pl-genco-flags: " << kGencoFlags << "\n// pl-compiler: " << __clang_version__ << "\n";
     if (tuned_wide(log_n, f_mode)) o << "#define PL_SC_MINW 3\n#define PL_SC_F_BITOP3 1\n";
-    // Exact-f codes with 128 channel slots per lane (n >= 128) at 3 waves per SIMD: the register
-    // cap spills part of the channel to scratch, which costs less than the occupancy it buys
-    // (the f's fp64 chains wait on latency at 2 waves).  Same-process A/B at (512,1024), bs =
-    // 65536 (profiles/r04d_sc_exact_ab.txt): 1.153 ms at 3 waves, 1.148 at 4, 1.295 at 2.
-    if (f_mode == PL_F_EXACT && log_n >= 7) o << "#define PL_SC_MINW 3\n";
+    // Exact-f codes with 128 channel slots per lane (n >= 128) at 3 waves per SIMD (the f's fp64
+    // chains wait on latency at 2 waves; same-process A/B at (512,1024), bs = 65536,
+    // profiles/r04d_sc_exact_ab.txt: 1.153 ms at 3 waves, 1.148 at 4, 1.295 at 2).  The 128 channel
+    // registers did not fit under that cap: 129 VGPRs were spilled to scratch (194 scratch
+    // instructions per wave, ~0.5 GB of scratch traffic per launch).  Round 5: the stage-(n/2)
+    // buffer in VGPRs and the channel read once per half (PL_SC_ROOT_MODE 1, whose second read the
+    // caches serve -- a second load latency, cheap against this kernel's ~1 ms): 8 spills,
+    // 13 scratch instructions per wave; same-process A/B (profiles/r05c_sc_exact_ab_*.txt)
+    // 0.9155 vs 0.9469 ms at (512,1024), 0.1801 vs 0.1979 ms at (128,256).
+    if (f_mode == PL_F_EXACT && log_n >= 7) o << "#define PL_SC_MINW 3\n#define PL_SC_ROOT_MODE 1\n";
     const int G = 1 << lg, NS = n >> lg;
     if (NS == 64) o << "#define PL_SC_SIM 1\n";  // the fused Monte-Carlo entry (sc_static.h OUT_SIM)
     std::string body = kStaticSrc;

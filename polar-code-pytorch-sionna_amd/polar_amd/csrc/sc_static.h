@@ -1257,7 +1257,8 @@ __device__ __forceinline__ void decode(const float* __restrict__ llr, int64_t bs
                                        const int32_t* __restrict__ info_loc, int k, float lmax,
                                        uint32_t* __restrict__ ulds, const uint32_t* __restrict__ ref = nullptr,
                                        const SimArgs* sa = nullptr) {
-    static_assert(OUT < OUT_CNT || (!PL_SC_PERSIST && !PL_SC_STAMPS && PL_SC_ROOT_MODE == 0), "OUT_CNT / OUT_SIM: plain decoder only");
+    static_assert(OUT < OUT_CNT || (!PL_SC_PERSIST && !PL_SC_STAMPS && (PL_SC_ROOT_MODE == 0 || OUT == OUT_CNT)),
+                  "OUT_CNT / OUT_SIM: plain decoder only (OUT_CNT also with the stage-(n/2) root of PL_SC_ROOT_MODE 1)");
     constexpr int N = C::N, G = C::G, LG = C::LOG_G, NS = C::NS, CW = 64 / G;
     constexpr int WPL = (NS + 31) / 32;
     // the wave index is wave-uniform: as an SGPR value all batch/row address math is scalar
@@ -1561,7 +1562,7 @@ __device__ __forceinline__ void decode_staged(const float* __restrict__ llr, int
 #define PL_SC_PERSIST_BPC 2  // resident blocks per CU the launcher gives a persistent kernel
 #endif
 // decode + error count against packed reference bits (pl_sc_decode_count); plain decoder only
-#if PL_SC_PERSIST || PL_SC_STAMPS || PL_SC_ROOT_MODE
+#if PL_SC_PERSIST || PL_SC_STAMPS
 #define PL_SC_CNT_ENTRY(CODE)
 #else
 #define PL_SC_CNT_ENTRY(CODE)                                                                                \

@@ -754,10 +754,10 @@ __device__ __forceinline__ void vnode64(const St& t, const Cw& w, const float* c
 // per path), then the y side and the node's f/g.  The X2 kernel's register budget (128 VGPRs):
 // both sides at once hold 32 channel values and 16 doubles per path step, which spilled.  The same
 // f/g operands and operations per element as vnode64, so the same values.
-template <int Q, int FM>
+template <int Q, int QE, int FM>  // levels Q down to QE of one side
 __device__ __forceinline__ void vside_levels(double* v, const uint32_t* bp, const int* wb, int j, int side,
                                              uint32_t gmask, double lmax) {
-    if constexpr (Q >= 0) {
+    if constexpr (Q >= QE && Q >= 0) {
         constexpr int h = 1 << Q;
         if ((gmask >> Q) & 1u) {
             const uint32_t* wq = bp + wb[Q] + side;
@@ -767,7 +767,7 @@ __device__ __forceinline__ void vside_levels(double* v, const uint32_t* bp, cons
 #pragma unroll
             for (int m = 0; m < h; ++m) v[m] = f_op<FM>(v[m], v[m + h], lmax);
         }
-        vside_levels<Q - 1, FM>(v, bp, wb, j, side, gmask, lmax);
+        vside_levels<Q - 1, QE, FM>(v, bp, wb, j, side, gmask, lmax);
     }
 }
 template <int L, int V, int FM>
@@ -788,7 +788,7 @@ __device__ __forceinline__ void vnode64_ns0(const St& t, const Cw& w, const floa
             const uint32_t* wq = bp + wb[V - 1] + side;
 #pragma unroll
             for (int m = 0; m < H; ++m) v[m] = g_op((double)c[m], (double)c[m + H], (wq[2 * m] >> j) & 1u);
-            vside_levels<V - 2, FM>(v, bp, wb, j, side, gmask, t.lmax);  // levels V-2 .. 1 (level 0 below)
+            vside_levels<V - 2, 1, FM>(v, bp, wb, j, side, gmask, t.lmax);  // levels V-2 .. 1 (level 0 below)
 #if PL_SCL_C7
             if (w7) {
                 double* e = reinterpret_cast<double*>(&vc->v7[it * L + p]) + 2 * side;

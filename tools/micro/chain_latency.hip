@@ -57,12 +57,14 @@ __global__ __launch_bounds__(64) void c_bperm(float* out, float a, unsigned long
 __global__ __launch_bounds__(64) void c_empty(float* out, float a, unsigned long long* tm) {
     if (a > 1e30f) out[threadIdx.x] = a + (float)(tm != nullptr);
 }
-// one dependent global load chain (pointer chasing in a 4 MB buffer: L2-resident after the first pass)
+// one dependent global load chain (pointer chasing in a 4 MB ring at word offset kRing of the
+// buffer, L2-resident after the first pass; the other kernels write words [0, 65536) only)
+constexpr unsigned kRing = 1u << 21, kRingWords = 1u << 20;
 __global__ __launch_bounds__(64) void c_gload(float* out, float a, unsigned long long* tm) {
-    const unsigned* p = reinterpret_cast<const unsigned*>(out);
+    const unsigned* p = reinterpret_cast<const unsigned*>(out) + kRing;
     unsigned x = threadIdx.x;
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    for (int it = 0; it < ITER / 16; ++it) x = __builtin_nontemporal_load(p + x) ^ (unsigned)(a > 1e30f);
+    for (int it = 0; it < ITER / 16; ++it) x = __builtin_nontemporal_load(p + (x & (kRingWords - 1))) ^ (unsigned)(a > 1e30f);
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     out[(1 << 20) + threadIdx.x] = (float)x + a;
     if (threadIdx.x == 0) *tm = t1 - t0;
@@ -83,6 +85,15 @@ __global__ __launch_bounds__(64) void c_clock(float* out, float a, unsigned long
 
 typedef void (*Kern)(float*, float, unsigned long long*);
 
+#define CK(x)                                                                                  \
+    do {                                                                                       \
+        hipError_t e_ = (x);                                                                   \
+        if (e_ != hipSuccess) {                                                                \
+            printf("HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__);      \
+            return 1;                                                                          \
+        }                                                                                      \
+    } while (0)
+
 int main() {
     const struct {
         const char* name;
@@ -95,10 +106,10 @@ int main() {
               {"ds_read_b32", c_lds, ITER}, {"ds_bpermute_b32", c_bperm, ITER}, {"global_load (L2)", c_gload, ITER / 16}};
     float* buf;
     if (hipMalloc(&buf, (size_t)(1 << 22) * sizeof(float)) != hipSuccess) return 1;
-    {  // pointer-chase ring in the first 1M words: x -> (x * 4093 + 64) mod 2^20
-        unsigned* h = new unsigned[1 << 20];
-        for (unsigned i = 0; i < (1u << 20); ++i) h[i] = (i * 4093u + 64u) & ((1u << 20) - 1u);
-        (void)hipMemcpy(buf, h, (size_t)(1 << 20) * 4, hipMemcpyHostToDevice);
+    {  // pointer-chase ring at word kRing: x -> (x * 4093 + 64) mod 2^20 (indices masked in the kernel too)
+        unsigned* h = new unsigned[kRingWords];
+        for (unsigned i = 0; i < kRingWords; ++i) h[i] = (i * 4093u + 64u) & (kRingWords - 1u);
+        CK(hipMemcpy(buf + kRing, h, (size_t)kRingWords * 4, hipMemcpyHostToDevice));
         delete[] h;
     }
     unsigned long long* tmd;
@@ -117,13 +128,14 @@ int main() {
             hipLaunchKernelGGL(c_add_f32, dim3(1024), dim3(64), 0, 0, buf, 1.0001f, tmd + 1);
             (void)hipEventRecord(e0);
             hipLaunchKernelGGL(k.k, dim3(1), dim3(64), 0, 0, buf, 1.0001f, tmd);
+            CK(hipGetLastError());
             (void)hipEventRecord(e1);
-            (void)hipEventSynchronize(e1);
+            CK(hipEventSynchronize(e1));
             float t = 0;
             (void)hipEventElapsedTime(&t, e0, e1);
             best = t < best ? t : best;
             unsigned long long c = 0;
-            (void)hipMemcpy(&c, tmd, 8, hipMemcpyDeviceToHost);
+            CK(hipMemcpy(&c, tmd, 8, hipMemcpyDeviceToHost));
             cyc = c < cyc ? c : cyc;
         }
         printf("%-24s %7.2f s_memtime cycles per dependent instruction (one wave; %.4f ms incl. launch)\n",
@@ -135,8 +147,9 @@ int main() {
         for (int i = 0; i < 100; ++i) hipLaunchKernelGGL(c_empty, dim3(blocks), dim3(64), 0, 0, buf, 1.0f, tmd);
         (void)hipEventRecord(e0);
         for (int i = 0; i < N; ++i) hipLaunchKernelGGL(c_empty, dim3(blocks), dim3(64), 0, 0, buf, 1.0f, tmd);
+        CK(hipGetLastError());
         (void)hipEventRecord(e1);
-        (void)hipEventSynchronize(e1);
+        CK(hipEventSynchronize(e1));
         float t = 0;
         (void)hipEventElapsedTime(&t, e0, e1);
         printf("empty kernel, %4d blocks   %.3f us per back-to-back launch\n", blocks, t * 1e3 / N);
@@ -145,9 +158,10 @@ int main() {
     {
         hipLaunchKernelGGL(c_add_f32, dim3(1024), dim3(64), 0, 0, buf, 1.0001f, tmd + 1);
         hipLaunchKernelGGL(c_clock, dim3(1), dim3(64), 0, 0, buf, 1.0001f, tmd);
-        (void)hipDeviceSynchronize();
+        CK(hipGetLastError());
+        CK(hipDeviceSynchronize());
         unsigned long long c[2] = {0, 0};
-        (void)hipMemcpy(c, tmd, 16, hipMemcpyDeviceToHost);
+        CK(hipMemcpy(c, tmd, 16, hipMemcpyDeviceToHost));
         printf("s_memtime clock: %.4f GHz (%llu cycles in %llu ticks of s_memrealtime at 100 MHz)\n",
                (double)c[0] / ((double)c[1] * 10.0), c[0], c[1]);
     }

@@ -125,6 +125,23 @@ KA(k_addudpp, F_ADDUDPP)
         out[blockIdx.x * 64 + threadIdx.x] = s;                                                          \
     }
 KV(k_cndmask, F_CNDM)
+// v_cndmask_b32_e64 with an SGPR-pair mask (the form the kernels' selects mostly take)
+__global__ __launch_bounds__(64) void k_cndmask64(float* out, float a) {
+    float x[8];
+    for (int i = 0; i < 8; ++i) x[i] = threadIdx.x * 0.001f + i;
+    const unsigned long long msk = 0x5555555555555555ull;  // a constant: materialised in an SGPR pair
+    for (int it = 0; it < ITER; ++it) {
+        asm volatile("v_cndmask_b32_e64 %0, %0, %4, %5\n v_cndmask_b32_e64 %1, %1, %4, %5\n"
+                     " v_cndmask_b32_e64 %2, %2, %4, %5\n v_cndmask_b32_e64 %3, %3, %4, %5"
+                     : "+v"(x[0]), "+v"(x[1]), "+v"(x[2]), "+v"(x[3]) : "v"(a), "s"(msk));
+        asm volatile("v_cndmask_b32_e64 %0, %0, %4, %5\n v_cndmask_b32_e64 %1, %1, %4, %5\n"
+                     " v_cndmask_b32_e64 %2, %2, %4, %5\n v_cndmask_b32_e64 %3, %3, %4, %5"
+                     : "+v"(x[4]), "+v"(x[5]), "+v"(x[6]), "+v"(x[7]) : "v"(a), "s"(msk));
+    }
+    float s = 0;
+    for (int i = 0; i < 8; ++i) s += x[i];
+    out[blockIdx.x * 64 + threadIdx.x] = s;
+}
 KV(k_cmpeq, F_CMPEQ)
 // v_pk_add_f32 on 64-bit register pairs (two results per instruction)
 __global__ __launch_bounds__(64) void k_pkadd(float* out, float a) {
@@ -157,7 +174,8 @@ int main() {
               {"v_alignbit_b32", k_alignbit}, {"v_lshlrev_b32", k_lshl}, {"v_lshrrev_b32", k_lshr},
               {"v_bfe_u32", k_bfe}, {"v_and_b32", k_and}, {"v_mov_b32", k_mov}, {"v_cvt_f32_ubyte0", k_cvtub},
               {"v_bcnt_u32_b32", k_bcnt}, {"v_xor_b32_dpp", k_xordpp}, {"v_and_b32_dpp", k_anddpp},
-              {"v_min_u32_dpp", k_minudpp}, {"v_add_u32_dpp", k_addudpp}, {"v_cndmask_b32", k_cndmask},
+              {"v_min_u32_dpp", k_minudpp}, {"v_add_u32_dpp", k_addudpp}, {"v_cndmask_b32_vcc", k_cndmask},
+              {"v_cndmask_b32", k_cndmask64},
               {"v_cmp_eq_f32", k_cmpeq}};
     const int blocks = 256 * 4 * 8;  // 8 waves per SIMD
     float* out;
