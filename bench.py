@@ -49,6 +49,9 @@ def parse():
                     help="distinct resident batches the steps cycle through (default 3 SC, 1 SCL)")
     ap.add_argument("--decoder", choices=["sc", "scl"], default="sc")
     ap.add_argument("--list-size", type=int, default=8)
+    ap.add_argument("--fmode", type=int, default=0, choices=[0, 1],
+                    help="f of the decoder: 0 min-sum (x_run SC_Dec / SCL_Dec, the headline), 1 the exact boxplus f "
+                         "(my_sn SC_Dec / SCL_Dec; profiling runs)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sim-iteration", action="store_true",
@@ -376,7 +379,8 @@ def valu_roofline(tag, kern_ms):
     out = {"bound": "valu_issue", "unit": "us of VALU issue per SIMD per launch", "kernel_ms": round(kern_ms, 5),
            "valu_instr_per_launch": v["valu_per_launch"], "counter_files": v.get("source"),
            "isa_sha": v.get("isa_sha")}
-    if v.get("isa_sha") != current_isa_sha(tag):
+    pin = current_isa_sha(tag)
+    if (v.get("isa_sha") != pin) if pin else (v.get("src_hash") != library_src_hash()):
         out.update({"stale": True, "frac": None, "frac_lo": None, "frac_hi": None})
         return out
     ns = v["issue_ns_simd_per_launch"]
@@ -432,7 +436,7 @@ def main():
     fp = polar_amd.reference_frozen_pos(k, n)
     mask = polar_amd.frozen_mask(fp, n)
     L = a.list_size if a.decoder == "scl" else 1
-    plan = _lib.Plan(n, mask, L, _lib.PL_F_MINSUM, device=dev)
+    plan = _lib.Plan(n, mask, L, a.fmode, device=dev)
     gen = torch.Generator(device=dev).manual_seed(42 + rank)
     model = channel.System_AWGN_model(n, k, channel.GpuEncoder(fp, n), None, device=dev, generator=gen)
     R = max(1, a.buffers)
@@ -496,12 +500,12 @@ def main():
     value = total_cw / wall / 1e6
     bytes_per_launch = bs * (4 * n + 4 * k)
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-    tag = f"{a.decoder}_k{k}_n{n}_bs{bs}" + (f"_L{L}" if L > 1 else "")
+    tag = f"{a.decoder}{'_exact' if a.fmode == 1 else ''}_k{k}_n{n}_bs{bs}" + (f"_L{L}" if L > 1 else "")
     sim_it = None
-    if a.decoder == "sc" and not a.no_sim_iteration:
+    if a.decoder == "sc" and a.fmode == 0 and not a.no_sim_iteration:
         sim_it = sim_iteration(plan, fp, k, n, bs, a.ebno, dev)
     configs = None
-    if a.decoder == "sc" and not a.no_configs and (k, n, bs) == (512, 1024, 65536):
+    if a.decoder == "sc" and a.fmode == 0 and not a.no_configs and (k, n, bs) == (512, 1024, 65536):
         # BASELINE.json configs[1] (k=128, n=256, bs=4096, SC) and configs[3] (k=512, n=1024,
         # L=8, bs=8192, SCL) on this GPU, after the headline's timed region
         c1, _, p1, l1, _ = config_line("sc", 128, 256, 4096, 1, a.ebno, dev, rank, 2000, 200)
@@ -518,11 +522,12 @@ def main():
             cx["roofline_valu"] = rv
         configs = {"configs_1": c1, "configs_3": c3, "mysn_sc_exact": cx}
     cpu = None
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.fmode == 0:
         cpu = cpu_baseline(llr.cpu().numpy(), fp.numpy(), k, n, a.decoder, L, a.cpu_seconds)
     if rank == 0:
         line = {
-            "metric": METRIC if a.decoder == "sc" else f"Mcodewords/s, SCL L={L} n={n}",
+            "metric": (METRIC if a.fmode == 0 else "Mcodewords/s, exact-boxplus SC (my_sn SC_Dec)") if a.decoder == "sc"
+                      else f"Mcodewords/s, SCL L={L} n={n}",
             "value": round(value, 4),
             "unit": "Mcodewords/s",
             "n_gpus": world,

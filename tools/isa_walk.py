@@ -166,7 +166,19 @@ CAL_MAP = {
     "v_mad_u32_u24": "v_bitop3_b32", "v_lshl_or_b32": "v_bitop3_b32", "v_lshl_add_u32": "v_bitop3_b32",
     "v_add3_u32": "v_bitop3_b32", "v_not_b32": "v_xor_b32", "v_max_f32": "v_min_f32", "v_min_f32": "v_min_f32",
     "v_sub_f32": "v_add_f32", "v_mul_f32": "v_mul_f32", "v_cmp_gt_u32": "v_cmp_eq_f32", "v_cmp_lt_u32": "v_cmp_eq_f32",
+    "v_lshlrev_b16": "v_lshlrev_b32", "v_bitop3_b16": "v_bitop3_b32", "v_bfrev_b32": "v_bfe_u32",
+    "v_cmp_gt_i64": "v_add_f64", "v_lshlrev_b64": "v_add_f64", "v_subrev_u32": "v_add_u32", "v_min3_u32": "v_min3_f32",
+    "v_xor_b32_sdwa": "v_xor_b32_dpp", "v_lshlrev_b32_sdwa": "v_xor_b32_dpp",
+    # fp64 and conversions (the exact-f kernels)
+    "v_fma_f64": "v_fma_f64", "v_fmac_f64": "v_fma_f64", "v_mul_f64": "v_mul_f64", "v_add_f64": "v_add_f64",
+    "v_ldexp_f64": "v_mul_f64", "v_cvt_f32_f64": "v_cvt_f32_f64+f64_f32", "v_cvt_f64_f32": "v_cvt_f32_f64+f64_f32",
+    "v_cvt_f64_i32": "v_cvt_f32_f64+f64_f32", "v_cmp_ngt_f32": "v_cmp_eq_f32", "v_cmp_gt_f32": "v_cmp_eq_f32",
+    "v_cmp_gt_i32": "v_cmp_eq_f32", "v_sub_f32_dpp": "v_add_f32_dpp", "v_subrev_f32_dpp": "v_add_f32_dpp",
+    "v_max_f32": "v_min_f32", "v_med3_f32": "v_med3_f32", "v_cmp_nlt_f32": "v_cmp_eq_f32",
 }
+# VOP2 v_cndmask_b32_e32 reads VCC implicitly: the micro measures that form apart (9.4 ns at 8 waves
+# per SIMD, against 1.8 ns for the VOP3 form with an SGPR-pair mask -- r05c_valu_cycles.txt)
+E32_FORM = {"v_cndmask_b32_e32": "v_cndmask_b32_vcc"}
 
 
 def base_mnemonic(m):
@@ -365,7 +377,7 @@ def record_valu(asm, tag, cal_path, sq_valu_per_wave=None, waves_per_launch=None
         if unit(m) != "valu":
             continue
         b = base_mnemonic(m)
-        form = CAL_MAP.get(b)
+        form = E32_FORM.get(m) if m in E32_FORM and E32_FORM[m] in cal else CAL_MAP.get(b)
         cost = cal.get(form) if form else None
         by[m] = [c, form, cost]
         if cost is None:
@@ -373,8 +385,8 @@ def record_valu(asm, tag, cal_path, sq_valu_per_wave=None, waves_per_launch=None
         else:
             mapped_ns += c * cost
     walk_valu = sum(c for m, c in h.items() if unit(m) == "valu")
-    lo_c = min(v for k, v in cal.items() if k != "v_exp_f32")
-    hi_c = max(v for k, v in cal.items() if k != "v_exp_f32")
+    plain = [v for k, v in cal.items() if k != "v_exp_f32" and not k.endswith("_vcc")]
+    lo_c, hi_c = min(plain), max(plain)  # the rest: between the cheapest and the dearest plain form
     resid = (sq_valu_per_wave - walk_valu) if sq_valu_per_wave is not None else 0.0
     un = sum(unmapped.values())
     from polar_amd import build as _b
@@ -449,7 +461,8 @@ def main():
         tag = a.tag or f"sc_k{a.k}_n{a.n}_bs{a.bs}"
         vj = json.load(open(os.path.join(ROOT, "profiles", "valu.json")))
         sq = vj.get(tag, {}).get("per_wave", {}).get("INSTS_VALU")
-        rec = record_valu(asm, tag, a.cal, sq, vj.get(tag, {}).get("waves_per_launch"), a.cpw)
+        waves = vj.get(tag, {}).get("waves_per_launch") or (a.bs // a.cpw if a.cpw else None)
+        rec = record_valu(asm, tag, a.cal, sq, waves, a.cpw)
         print(json.dumps({k: rec[k] for k in ("valu_per_wave_walk", "valu_per_wave_sq", "issue_ns_per_wave", "unmapped")}))
         return
     if a.cmd == "chain":

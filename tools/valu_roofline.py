@@ -25,9 +25,11 @@ import os
 import re
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {"sc": "pl_sc_static_f32", "scl": "scl_tree_kernel<8, 4, 0, false>"}
-KEYS = {"sc": "sc_k512_n1024_bs65536", "scl": "scl_k512_n1024_bs8192_L8"}
-PINS = {"sc": "sc_k512_n1024_minsum", "scl": "scl_L8_n1024_minsum"}
+import sys  # noqa: E402
+sys.path.insert(0, os.path.join(ROOT, "polar-code-pytorch-sionna_amd"))
+KERNELS = {"sc": "pl_sc_static_f32", "scl": "scl_tree_kernel<8, 4, 0, false>", "scx": "pl_sc_static_f32"}
+KEYS = {"sc": "sc_k512_n1024_bs65536", "scl": "scl_k512_n1024_bs8192_L8", "scx": "sc_exact_k512_n1024_bs65536"}
+PINS = {"sc": "sc_k512_n1024_minsum", "scl": "scl_L8_n1024_minsum", "scx": None}  # scx: stale by source hash
 # counter class -> calibration form(s) whose cost it carries
 CLASSES = {"SQ_INSTS_VALU_ADD_F32": "v_add_f32", "SQ_INSTS_VALU_MUL_F32": "v_mul_f32",
            "SQ_INSTS_VALU_FMA_F32": "v_fma_f32", "SQ_INSTS_VALU_TRANS_F32": "v_exp_f32",
@@ -81,8 +83,11 @@ def main():
         classes = {c: merged.get(c, 0.0) for c in CLASSES}
         other = total - sum(classes.values())
         known_ns = sum(classes[c] * cal[CLASSES[c]] for c in classes)
+        from polar_amd import build as _b
+        keep = vj.get(KEYS[dec], {}).get("static")  # tools/isa_walk.py valu: kept across SQ refreshes
         vj[KEYS[dec]] = {
-            "kernel": KERNELS[dec], "isa_sha": pins[PINS[dec]]["sha"], "dispatches": n, "waves_per_launch": waves,
+            "kernel": KERNELS[dec], "isa_sha": pins[PINS[dec]]["sha"] if PINS[dec] else None,
+            "src_hash": _b.source_hash(), "dispatches": n, "waves_per_launch": waves,
             "valu_per_launch": total, "class_counts_per_launch": classes, "other_per_launch": other,
             "issue_ns_simd_per_launch": {"classified": known_ns, "other_lo": other * cal[OTHER[0]],
                                          "other_hi": other * cal[OTHER[1]]},
@@ -91,6 +96,8 @@ def main():
             "calibration_ns": {CLASSES[c]: cal[CLASSES[c]] for c in CLASSES} | {f: cal[f] for f in OTHER},
             "source": [f"profiles/{a.tag}_sq_{dec}_{p}.csv" for p in "ABC"] + [a.cal],
         }
+        if keep is not None:
+            vj[KEYS[dec]]["static"] = keep
         print(dec, json.dumps(vj[KEYS[dec]]["issue_ns_simd_per_launch"]), "per wave VALU",
               round(total / waves, 1), "other", round(other / waves, 1))
     json.dump(vj, open(vj_path, "w"), indent=1)
