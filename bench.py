@@ -360,7 +360,7 @@ def valu_roofline(tag, kern_ms):
                "method": "per-mnemonic: the walked instruction stream (tools/isa_walk.py) x calibrated issue cost per "
                          "form (tools/micro/valu_cycles.hip); the residual against SQ_INSTS_VALU as a cost range",
                "valu_per_wave_walk": st["valu_per_wave_walk"], "valu_per_wave_sq": st["valu_per_wave_sq"],
-               "calibration": st["calibration"], "stale": not fresh}
+               "counter_files": v.get("source"), "calibration": st["calibration"], "stale": not fresh}
         if not fresh:
             out.update({"frac": None, "frac_lo": None, "frac_hi": None})
             return out
