@@ -365,11 +365,22 @@ def isa_sha(asm, kernel="pl_sc_static_f32"):
     return t.isa_summary(asm, lambda nm: nm == kernel)[kernel]["sha"]
 
 
-def record_valu(asm, tag, cal_path, sq_valu_per_wave=None, waves_per_launch=None, codewords_per_wave=None):
+def record_valu(asm, tag, cal_path, sq_valu_per_wave=None, waves_per_launch=None, codewords_per_wave=None,
+                normalise=False):
     """profiles/valu.json[tag]["static"]: the walked stream's VALU per wave by mnemonic, each with
     its calibrated issue cost (tools/micro/valu_cycles.hip), and the residual against the SQ
     counter (instructions the walk does not see: rare fallbacks) carried as a cost range."""
     cal = calibration(cal_path)
+    # the calibration kernels and the decode kernel run at different clocks (DVFS: the fp64 forms at
+    # ~2.13 GHz, the min-sum SC kernel at ~2.42): costs go to cycles at their own clock and back to
+    # ns at the decode kernel's (profiles/clocks.json, tools/kernel_clock.py), when both are known
+    # (off by default: the clocks come from profiled runs, whose kernels run ~10-15 % slower than the
+    # clean calibration run; --clock-normalise applies them)
+    clk_path = os.path.join(ROOT, "profiles", "clocks.json")
+    clk = json.load(open(clk_path)) if (normalise and os.path.exists(clk_path)) else {}
+    f_dec = clk.get("kernels_ghz", {}).get(tag)
+    if f_dec:
+        cal = {f: ns * clk["calibration_ghz"].get(f, f_dec) / f_dec for f, ns in cal.items()}
     h, ins, tr = dynamic_histogram(asm, "pl_sc_static_f32")
     by = {}
     mapped_ns, unmapped = 0.0, Counter()
@@ -390,7 +401,8 @@ def record_valu(asm, tag, cal_path, sq_valu_per_wave=None, waves_per_launch=None
     resid = (sq_valu_per_wave - walk_valu) if sq_valu_per_wave is not None else 0.0
     un = sum(unmapped.values())
     from polar_amd import build as _b
-    rec = {"isa_sha": isa_sha(asm), "src_hash": _b.source_hash(), "calibration": cal_path, "valu_per_wave_walk": walk_valu,
+    rec = {"isa_sha": isa_sha(asm), "src_hash": _b.source_hash(), "calibration": cal_path,
+           "clock_normalised": bool(f_dec), "kernel_clock_ghz": f_dec, "valu_per_wave_walk": walk_valu,
            "valu_per_wave_sq": sq_valu_per_wave, "residual_per_wave": round(resid, 1),
            "issue_ns_per_wave": {"mapped": round(mapped_ns, 1),
                                  "rest_lo": round((un + max(resid, 0)) * lo_c, 1),
@@ -444,6 +456,7 @@ def main():
     ap.add_argument("--tag", default=None, help="valu.json / latency.json key")
     ap.add_argument("--bs", type=int, default=65536)
     ap.add_argument("--cpw", type=int, default=None, help="codewords per wave (64 / lanes per codeword)")
+    ap.add_argument("--clock-normalise", action="store_true", help="valu: costs onto the decode kernel's clock (profiles/clocks.json)")
     a = ap.parse_args()
     asm = open(a.asm).read() if a.asm else kernel_asm(a.k, a.n, a.fm)
     ins = parse(asm)
@@ -462,7 +475,7 @@ def main():
         vj = json.load(open(os.path.join(ROOT, "profiles", "valu.json")))
         sq = vj.get(tag, {}).get("per_wave", {}).get("INSTS_VALU")
         waves = vj.get(tag, {}).get("waves_per_launch") or (a.bs // a.cpw if a.cpw else None)
-        rec = record_valu(asm, tag, a.cal, sq, waves, a.cpw)
+        rec = record_valu(asm, tag, a.cal, sq, waves, a.cpw, a.clock_normalise)
         print(json.dumps({k: rec[k] for k in ("valu_per_wave_walk", "valu_per_wave_sq", "issue_ns_per_wave", "unmapped")}))
         return
     if a.cmd == "chain":
