@@ -144,7 +144,18 @@ def unit(m):
 
 
 def histogram(ins, trace):
-    return Counter(ins[i][1].split()[0] for i in trace)
+    """Mnemonic counts of the walked stream; a VOP2 select that directly follows another VOP2 select
+    (the VALU before it) is counted as "v_cndmask_b32_e32:b2b": only that pairing issues slowly
+    (tools/micro/cndmask_forms.hip)."""
+    h, prev = Counter(), None
+    for i in trace:
+        m = ins[i][1].split()[0]
+        if m.startswith("v_"):
+            h[m + ":b2b" if m == prev == "v_cndmask_b32_e32" else m] += 1
+            prev = m
+        else:
+            h[m] += 1
+    return h
 
 
 # mnemonic (suffix-stripped) -> calibration form of tools/micro/valu_cycles.hip
@@ -176,9 +187,14 @@ CAL_MAP = {
     "v_cmp_gt_i32": "v_cmp_eq_f32", "v_sub_f32_dpp": "v_add_f32_dpp", "v_subrev_f32_dpp": "v_add_f32_dpp",
     "v_max_f32": "v_min_f32", "v_med3_f32": "v_med3_f32", "v_cmp_nlt_f32": "v_cmp_eq_f32",
 }
-# VOP2 v_cndmask_b32_e32 reads VCC implicitly: the micro measures that form apart (9.4 ns at 8 waves
-# per SIMD, against 1.8 ns for the VOP3 form with an SGPR-pair mask -- r05c_valu_cycles.txt)
-E32_FORM = {"v_cndmask_b32_e32": "v_cndmask_b32_vcc"}
+# VOP2 v_cndmask_b32_e32 (mask = VCC, implicit).  valu_cycles.hip times a run of them back to back
+# at 9.4 ns per instruction (8 waves per SIMD), against 1.8 ns for the VOP3 form; in the kernels'
+# patterns they cost what the VOP3 form costs (tools/micro/cndmask_forms.hip,
+# profiles/r05f_cndmask_forms.txt: after a v_cmp 1.58 vs 1.57 ns per instruction, one per three adds
+# 1.057 vs 1.056).  Two back to back after a v_cmp (the min/max swaps of the exact f: "cmp_sel2")
+# add ~2.5 ns to the second; those (":b2b", 232 per wave in the exact-f SC kernel) are costed as the
+# VOP3 form too, the difference below 0.5 % of that kernel's issue time.
+E32_FORM = {"v_cndmask_b32_e32": "v_cndmask_b32", "v_cndmask_b32_e32:b2b": "v_cndmask_b32"}
 
 
 def base_mnemonic(m):
