@@ -372,7 +372,8 @@ def valu_roofline(tag, kern_ms):
         out.update({"frac": round((lo + hi) / 2, 4), "frac_lo": round(lo, 4), "frac_hi": round(hi, 4),
                     "achieved": round((lo + hi) / 2 * kern_ms * 1e3, 2), "peak": round(kern_ms * 1e3, 2),
                     "wait_share_per_wave": round(v["per_wave"]["WAIT_ANY"] / v["per_wave"]["WAVE_CYCLES"], 4)
-                    if "per_wave" in v and "WAIT_ANY" in v["per_wave"] else None})
+                    if "per_wave" in v and "WAIT_ANY" in v["per_wave"] and v.get("isa_sha") in (None, st.get("isa_sha"))
+                    else None})  # the SQ pass's wait share, when it profiled this instruction stream
         return out
     if not v or "issue_ns_simd_per_launch" not in v:
         return None

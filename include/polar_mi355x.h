@@ -50,6 +50,9 @@ extern "C" {
 
 #define PL_F_MINSUM 0 /* f = sign*sign*min(|x|,|y|) on clipped inputs (polar_sc.py:46) */
 #define PL_F_EXACT 1  /* f = log(1+e^(x+y)) - log(e^x+e^y) (my_sn dec.py:39-43) */
+#define PL_F_WIDE_RANGE 0x100 /* pl_sc_source / pl_sc_specialize: or-ed into PL_F_EXACT, the code object
+                                 of plans whose llr_max exceeds 43 (full-range exp/log); without it,
+                                 the code object of plans with llr_max <= 43 */
 
 #define PL_PLAN_GENERIC 1u    /* pl_plan_create flag: never specialise the SC kernel */
 #define PL_PLAN_CACHE_ONLY 2u /* pl_plan_create flag: use a cached specialised kernel, never compile */
@@ -129,7 +132,8 @@ int pl_plan_kernel(const pl_plan* plan, int32_t* kind, char* path, size_t path_l
 
 /* Compile (or find) the specialised SC kernel of a code into cache_dir (NULL = default cache)
  * without touching a GPU; path (nullable) receives the code object file.  Used to pre-build the
- * kernels of known codes. */
+ * kernels of known codes.  f_mode: PL_F_MINSUM, PL_F_EXACT or PL_F_EXACT | PL_F_WIDE_RANGE (an
+ * exact-f plan picks one of the two by its llr_max). */
 int pl_sc_specialize(int32_t n, const uint8_t* frozen_mask, int32_t f_mode, const char* cache_dir,
                      char* path, size_t path_len);
 /* The HIP source of the specialised SC kernel of a code and its cache file name (what

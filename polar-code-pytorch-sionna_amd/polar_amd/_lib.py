@@ -16,6 +16,7 @@ LIB_PATH = os.path.join(_HERE, "libpolar_mi355x.so")
 
 PL_OK, PL_EINVAL, PL_EHIP, PL_ENOTSUP = 0, -1, -2, -3
 PL_F_MINSUM, PL_F_EXACT = 0, 1
+PL_F_WIDE_RANGE = 0x100  # sc_source / pl_sc_specialize: the exact-f code object of plans with llr_max > 43
 PL_OUT_F32, PL_OUT_U8 = 0, 1
 PL_PLAN_GENERIC, PL_PLAN_CACHE_ONLY, PL_PLAN_FAST_SCL, PL_PLAN_JIT = 1, 2, 4, 8
 PL_KERNEL_GENERIC, PL_KERNEL_SPECIALIZED, PL_KERNEL_SCL_SUBTREE = 0, 1, 2

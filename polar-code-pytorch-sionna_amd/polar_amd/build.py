@@ -244,10 +244,12 @@ def reference_codes():
     out += [(m, 0) for _, m in root_half_codes()]
     # tests/test_sc_gpu.py::test_sc_edge_cases: n = 64 with every position frozen (k = 0) and none (k = n)
     out += [(np.ones(64, dtype=np.uint8), 0), (np.zeros(64, dtype=np.uint8), 0)]
-    # tests/test_sc_gpu.py::test_sc_exact_large_llr_max_*: every n = 2, 4 code with k >= 1, exact f
+    # tests/test_sc_gpu.py::test_sc_exact_large_llr_max_*: every n = 2, 4 code with k >= 1, exact f,
+    # llr_max 60 and 80 (the full-range code object, PL_F_WIDE_RANGE) and the default 30
     for n in (2, 4):
         for code in range(1, 1 << n):
-            out.append((np.array([((code >> i) & 1) ^ 1 for i in range(n)], dtype=np.uint8), 1))
+            m = np.array([((code >> i) & 1) ^ 1 for i in range(n)], dtype=np.uint8)
+            out += [(m, 1), (m, 1 | 0x100)]
     uniq = {}
     for m, fm in out:
         uniq[(bytes(bytearray(m)), fm)] = (m, fm)

@@ -582,6 +582,21 @@ __device__ __forceinline__ float f_exact_wide(float x, float y, float lmax) {
 }
 // exp_cr's range |x| <= 87 holds for every argument f forms when llr_max <= 43 (|xc + yc| <= 86)
 constexpr float kExactFastLmax = 43.0f;
+// PL_EXF_RANGE: 0 = each f tests llr_max (a kernel for any plan), 1 = the fast forms only, 2 = the
+// full-range forms only.  The code-specialised SC kernels are built as 1 or 2 (jit.cpp: the plan's
+// llr_max <= 43 or not picks the code object), so their f carry no test and the lane-level f can be
+// inlined (sc_static.h PL_SC_FLANE_INLINE) without dragging the full-range path into the kernel.
+#ifndef PL_EXF_RANGE
+#define PL_EXF_RANGE 0
+#endif
+__device__ __forceinline__ bool wide_range(float lmax) {
+#if PL_EXF_RANGE == 0
+    return lmax > kExactFastLmax;
+#else
+    (void)lmax;
+    return PL_EXF_RANGE == 2;
+#endif
+}
 
 // clip(x, +-lmax) (dec.py:39-40) as one v_med3_f32 instead of the canonicalising v_max / v_min
 // pairs fminf(fmaxf(x, -lmax), lmax) compiles to (LLRs are never NaN: DESIGN.md section 7); the
@@ -611,10 +626,22 @@ __device__ __forceinline__ float uniform_l(float lmax) {
 
 // f of my_sn/fec/polar/dec.py:39-43 on clipped inputs, each operation rounded as the reference does.
 // Out of line: inlined into the fully unrolled specialised SC kernels (hundreds of f per lane) the
-// fp64 code made one (128,256) kernel take minutes to compile.
-__device__ __attribute__((noinline)) float f_exact(float x, float y, float lmax) {
+// fp64 code made one (128,256) kernel take minutes to compile.  PL_EXF_INLINE 1 inlines f_exact and
+// f_exact2 (fixed-range builds only, PL_EXF_RANGE != 0).
+#ifndef PL_EXF_INLINE
+#define PL_EXF_INLINE 0
+#endif
+#if PL_EXF_INLINE && PL_EXF_RANGE == 0
+#error "PL_EXF_INLINE needs PL_EXF_RANGE 1 or 2"
+#endif
+#if PL_EXF_INLINE
+#define PL_EXF_ATTR __attribute__((always_inline))
+#else
+#define PL_EXF_ATTR __attribute__((noinline))
+#endif
+__device__ PL_EXF_ATTR float f_exact(float x, float y, float lmax) {
     lmax = uniform_l(lmax);
-    if (lmax > kExactFastLmax) return f_exact_wide(x, y, lmax);
+    if (wide_range(lmax)) return f_exact_wide(x, y, lmax);
     const float xc = clip_l(x, lmax), yc = clip_l(y, lmax);
 #if PL_EXF_LEAN
     const double ex = exp_d(xc), ey = exp_d(yc);
@@ -633,9 +660,9 @@ __device__ __attribute__((noinline)) float f_exact(float x, float y, float lmax)
 struct f2 {
     float a, b;
 };
-__device__ __attribute__((noinline)) f2 f_exact2(float x0, float y0, float x1, float y1, float lmax) {
+__device__ PL_EXF_ATTR f2 f_exact2(float x0, float y0, float x1, float y1, float lmax) {
     lmax = uniform_l(lmax);
-    if (lmax > kExactFastLmax) return f2{f_exact_wide(x0, y0, lmax), f_exact_wide(x1, y1, lmax)};
+    if (wide_range(lmax)) return f2{f_exact_wide(x0, y0, lmax), f_exact_wide(x1, y1, lmax)};
     const float xc0 = clip_l(x0, lmax), yc0 = clip_l(y0, lmax);
     const float xc1 = clip_l(x1, lmax), yc1 = clip_l(y1, lmax);
 #if PL_EXF_LEAN

@@ -162,7 +162,10 @@ int mirror_lane(int G, int r) {
     return r < G / 2 ? mirror_lane(G / 2, r) : G - 1 - mirror_lane(G / 2, r - G / 2);
 }
 
-std::string static_source(int n, const uint8_t* frozen, int f_mode) {
+std::string static_source(int n, const uint8_t* frozen, int f_mode_in) {
+    // PL_F_WIDE_RANGE (exact f only): the code object of plans with llr_max > 43
+    const bool wide = (f_mode_in & PL_F_WIDE_RANGE) != 0;
+    const int f_mode = f_mode_in & ~PL_F_WIDE_RANGE;
     const int log_n = log2_exact(n), lg = static_log_g(log_n, f_mode);
     std::vector<uint8_t> nt = node_types(n, frozen);
     if (tuned_wide(log_n, f_mode)) {
@@ -187,6 +190,11 @@ std::string static_source(int n, const uint8_t* frozen, int f_mode) {
     // 13 scratch instructions per wave; same-process A/B (profiles/r05c_sc_exact_ab_*.txt)
     // 0.9155 vs 0.9469 ms at (512,1024), 0.1801 vs 0.1979 ms at (128,256).
     if (f_mode == PL_F_EXACT && log_n >= 7) o << "#define PL_SC_MINW 3\n#define PL_SC_ROOT_MODE 1\n";
+    // Exact f: one code object per llr_max range (exactf.h PL_EXF_RANGE), so no f tests llr_max
+    // and the lane-level f is inlined in the fast one (same-process A/B at (512,1024), bs = 65536,
+    // profiles/r05f_sc_exact_ab_1024.txt: 0.9181 ms with the test in every f, 0.8618 without,
+    // 0.8126 inlined; (128,256) 0.1802 / 0.1723 / 0.1705 ms).
+    if (f_mode == PL_F_EXACT) o << (wide ? "#define PL_EXF_RANGE 2\n" : "#define PL_EXF_RANGE 1\n#define PL_SC_FLANE_INLINE 1\n");
     const int G = 1 << lg, NS = n >> lg;
     if (NS == 64) o << "#define PL_SC_SIM 1\n";  // the fused Monte-Carlo entry (sc_static.h OUT_SIM)
     std::string body = kStaticSrc;
@@ -305,7 +313,8 @@ int specialize(int n, const uint8_t* frozen, int f_mode, const char* forced_dir,
 int attach_static(pl_plan* p, const uint8_t* frozen, bool allow_compile) {
     std::vector<char> image;
     std::string path;
-    int r = specialize(p->n, frozen, p->f_mode, nullptr, allow_compile, image, path);
+    const int fm = p->f_mode == PL_F_EXACT && p->llr_max > 43.0f ? (PL_F_EXACT | PL_F_WIDE_RANGE) : p->f_mode;
+    int r = specialize(p->n, frozen, fm, nullptr, allow_compile, image, path);
     if (r) return r;
     hipModule_t mod;
     r = check_hip(hipModuleLoadData(&mod, image.data()), "hipModuleLoadData(specialised SC kernel)");
@@ -453,7 +462,7 @@ extern "C" {
 
 int pl_sc_specialize(int32_t n, const uint8_t* frozen_mask, int32_t f_mode, const char* cache_dir, char* path_out,
                      size_t path_len) {
-    if (!frozen_mask || log2_exact(n) < 1 || log2_exact(n) > 11 || (f_mode != PL_F_MINSUM && f_mode != PL_F_EXACT)) {
+    if (!frozen_mask || log2_exact(n) < 1 || log2_exact(n) > 11 || (f_mode != PL_F_MINSUM && f_mode != PL_F_EXACT && f_mode != (PL_F_EXACT | PL_F_WIDE_RANGE))) {
         pl::set_error("pl_sc_specialize: bad arguments");
         return PL_EINVAL;
     }
@@ -470,7 +479,7 @@ int pl_sc_specialize(int32_t n, const uint8_t* frozen_mask, int32_t f_mode, cons
 
 int pl_sc_source(int32_t n, const uint8_t* frozen_mask, int32_t f_mode, char* src_out, size_t src_len,
                  size_t* src_size, char* name_out, size_t name_len) {
-    if (!frozen_mask || log2_exact(n) < 1 || log2_exact(n) > 11 || (f_mode != PL_F_MINSUM && f_mode != PL_F_EXACT)) {
+    if (!frozen_mask || log2_exact(n) < 1 || log2_exact(n) > 11 || (f_mode != PL_F_MINSUM && f_mode != PL_F_EXACT && f_mode != (PL_F_EXACT | PL_F_WIDE_RANGE))) {
         pl::set_error("pl_sc_source: bad arguments");
         return PL_EINVAL;
     }

@@ -366,10 +366,23 @@ __device__ uint32_t lnode(float a, const Lane& ln);
 // low element).  Every lane ends with the same bits as f_exact(x, y) -- each sum is commutative,
 // each transcendental correctly rounded -- so the replication the layout relies on holds.
 // 1 exp + 1 log per lane (S < G) or 2 + 1 (S = G) instead of 3 + 2.
+// Inlined, the lane-level f drops its call overhead (argument moves, the ABI's register
+// constraints); only with a fixed range (PL_EXF_RANGE != 0), where it has no full-range path.
+#ifndef PL_SC_FLANE_INLINE
+#define PL_SC_FLANE_INLINE 0
+#endif
+#if PL_SC_FLANE_INLINE && PL_EXF_RANGE == 0
+#error "PL_SC_FLANE_INLINE needs PL_EXF_RANGE 1 or 2"
+#endif
+#if PL_SC_FLANE_INLINE
+#define PL_FLANE_ATTR __attribute__((always_inline))
+#else
+#define PL_FLANE_ATTR __attribute__((noinline))
+#endif
 template <int S, bool TOP>
-__device__ __attribute__((noinline)) float f_lane_exact(float a, float y, uint32_t role31, float lmax) {
+__device__ PL_FLANE_ATTR float f_lane_exact(float a, float y, uint32_t role31, float lmax) {
     lmax = plx::uniform_l(lmax);
-    if (lmax > plx::kExactFastLmax) return plx::f_exact_wide(a, y, lmax);
+    if (plx::wide_range(lmax)) return plx::f_exact_wide(a, y, lmax);
     const float xc = plx::clip_l(a, lmax), yc = plx::clip_l(y, lmax);
     const bool A = (int32_t)role31 < 0;
     float arg;

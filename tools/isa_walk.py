@@ -66,7 +66,7 @@ def walk(ins):
     llr_max test's fast arm entered (s_cbranch_execnz after the s_xor_b64 of a saveexec) and its
     empty else arm skipped (after s_andn2_saveexec_b64).  Returns the instruction indices in order."""
     lab = {t: i for i, (k, t) in enumerate(ins) if k == "label"}
-    pc, trace, prev, cmp43 = 0, [], "", False
+    pc, trace, prev, cmp43, masks43 = 0, [], "", False, set()
     while pc < len(ins) and len(trace) < 10 ** 6:
         k, t = ins[pc]
         if k == "label":
@@ -77,6 +77,12 @@ def walk(ins):
         if m.startswith("v_cmp"):  # the exact f's range test: llr_max against 43.0 (0x422c0000)
             cmp43 = m.startswith("v_cmp_ngt_f32") and any(
                 ins[j][0] == "ins" and "0x422c0000" in ins[j][1] for j in range(max(0, pc - 6), pc))
+            mm = re.match(r"v_cmp_ngt_f32_e64 (s\[\d+:\d+\])", t)
+            if cmp43 and mm:  # the test hoisted into an SGPR pair (inlined f): each site ands it with exec
+                masks43.add(mm.group(1))
+        mm = re.match(r"s_and_b64 vcc, exec, (s\[\d+:\d+\])", t)
+        if mm:
+            cmp43 = mm.group(1) in masks43
         if m in ("s_endpgm", "s_setpc_b64"):
             break
         if m == "s_branch":
@@ -490,6 +496,8 @@ def main():
         tag = a.tag or f"sc_k{a.k}_n{a.n}_bs{a.bs}"
         vj = json.load(open(os.path.join(ROOT, "profiles", "valu.json")))
         sq = vj.get(tag, {}).get("per_wave", {}).get("INSTS_VALU")
+        if sq is not None and vj[tag].get("isa_sha") not in (None, isa_sha(asm)):
+            sq = None  # the SQ pass counted another instruction stream
         waves = vj.get(tag, {}).get("waves_per_launch") or (a.bs // a.cpw if a.cpw else None)
         rec = record_valu(asm, tag, a.cal, sq, waves, a.cpw, a.clock_normalise)
         print(json.dumps({k: rec[k] for k in ("valu_per_wave_walk", "valu_per_wave_sq", "issue_ns_per_wave", "unmapped")}))
