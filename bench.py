@@ -265,6 +265,35 @@ def config_line(decoder, k, n, bs, L, ebno, dev, rank, steps, warmup, fmode=0):
     return res, fn, plan, llr, out
 
 
+def graph_line(fn, steps, dev, chain_us=None):
+    """The same launches replayed from one captured HIP graph (polar_amd.ops.LaunchGraph): ms per
+    launch, and the graph's own launch floor (the same number of empty kernels replayed), which
+    replaces the eager floor in the critical-path bound."""
+    from polar_amd import ops
+    g = ops.LaunchGraph(fn, steps, dev)
+    x = torch.zeros(1, device=dev)
+    ge = ops.LaunchGraph(lambda: x.add_(1.0), steps, dev)
+
+    def per_launch(graph):
+        for _ in range(3):
+            graph.replay()
+        torch.cuda.synchronize(dev)
+        st = torch.cuda.current_stream(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(5):
+            graph.replay()
+        e1.record(st)
+        torch.cuda.synchronize(dev)
+        return e0.elapsed_time(e1) / (5 * graph.launches)
+    ms, floor_ms = per_launch(g), per_launch(ge)
+    out = {"kernel_ms": round(ms, 5), "launches_per_graph": steps, "launch_floor_us": round(floor_ms * 1e3, 3)}
+    if chain_us is not None:
+        bound = chain_us / 1e3 + floor_ms
+        out.update({"bound_ms": round(bound, 5), "frac": round(bound / ms, 4)})
+    return out
+
+
 def library_src_hash():
     """The source hash the loaded libpolar_mi355x.so was built from (pl_version)."""
     from polar_amd import _lib
@@ -509,8 +538,11 @@ def main():
     if a.decoder == "sc" and a.fmode == 0 and not a.no_configs and (k, n, bs) == (512, 1024, 65536):
         # BASELINE.json configs[1] (k=128, n=256, bs=4096, SC) and configs[3] (k=512, n=1024,
         # L=8, bs=8192, SCL) on this GPU, after the headline's timed region
-        c1, _, p1, l1, _ = config_line("sc", 128, 256, 4096, 1, a.ebno, dev, rank, 2000, 200)
+        c1, f1, p1, l1, _ = config_line("sc", 128, 256, 4096, 1, a.ebno, dev, rank, 2000, 200)
         c1["roofline_latency"] = latency_bound("sc_k128_n256", c1["kernel_ms"])
+        # the same launches replayed from a captured HIP graph (the launch gap of a small batch)
+        rl = c1["roofline_latency"]
+        c1["graph"] = graph_line(f1, 200, dev, rl.get("chain_us") if rl and not rl.get("stale") else None)
         c1["single_wave"] = latency_roofline(p1, l1, 128, 256, 4096, c1["kernel_ms"], dev)
         c3, _, _, _, _ = config_line("scl", 512, 1024, 8192, 8, a.ebno, dev, rank, 20, 3)
         rv = valu_roofline("scl_k512_n1024_bs8192_L8", c3["kernel_ms"])

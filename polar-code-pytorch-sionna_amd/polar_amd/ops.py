@@ -238,3 +238,30 @@ def count_errors(a, b, counts=None):
                                               ctypes.c_void_p(counts.data_ptr()), _lib.current_stream_ptr(a.device)),
                    "pl_count_errors")
     return counts
+
+
+class LaunchGraph:
+    """`launches` back-to-back calls of fn() (decodes of resident batches: ops.sc_decode /
+    scl_decode with `out` -- and for SCL `workspace` -- given, so nothing is allocated) captured
+    once into a HIP graph and replayed as one submission.  Small batches are launch-bound: at
+    (128,256) x 4096 a decode is ~7.5 us per launch issued one by one and ~6.5 us per launch
+    replayed (profiles/r05i_graph_time.txt; an empty kernel: ~3 us vs ~1.7 us).  The graph
+    holds the buffers' addresses: refill the same tensors in place between replays."""
+
+    def __init__(self, fn, launches, device=None):
+        if launches < 1:
+            raise ValueError("launches must be >= 1")
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.launches = int(launches)
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):  # one eager call first: plans load their code object lazily
+            fn()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.device(dev), torch.cuda.graph(self.graph):
+            for _ in range(self.launches):
+                fn()
+
+    def replay(self):
+        self.graph.replay()

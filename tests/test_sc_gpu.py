@@ -268,3 +268,32 @@ def test_plans_are_device_bound(pa):
     assert dec.plan(1).device == torch.device("cuda", 1)
     with pytest.raises(ValueError, match="device-bound"):
         ops.sc_decode(p0, x.cuda(1))
+
+
+def test_launch_graph_replays_bit_exact(pa):
+    """ops.LaunchGraph: back-to-back SC (specialised, configs[1] shape) and SCL (L = 8, with its
+    workspace) decodes of resident batches captured into one HIP graph; each replay leaves the
+    same bits as the eager calls, also after the inputs are refilled in place."""
+    from polar_amd import _lib, ops
+    g = np.random.default_rng(11)
+    fp = pa.reference_frozen_pos(128, 256)
+    plan = _plan(pa, fp, 256)
+    llr = torch.from_numpy(g.normal(0.0, 2.0, (4096, 256)).astype(np.float32)).cuda()
+    out = torch.empty((4096, 128), device="cuda")
+    lg = ops.LaunchGraph(lambda: ops.sc_decode(plan, llr, out=out), 3)
+    for _ in range(2):
+        out.zero_()
+        lg.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, ops.sc_decode(plan, llr)), "SC graph replay"
+        llr.copy_(torch.from_numpy(g.normal(0.0, 2.0, (4096, 256)).astype(np.float32)))
+    fp8 = pa.reference_frozen_pos(64, 128)
+    p8 = _lib.Plan(128, pa.frozen_mask(fp8, 128), 8, 0)
+    x = torch.from_numpy(g.normal(0.0, 2.0, (256, 128)).astype(np.float32)).cuda()
+    o8 = torch.empty((256, 64), device="cuda")
+    ws = ops.scl_workspace(p8, 256, x.device)
+    lg8 = ops.LaunchGraph(lambda: ops.scl_decode(p8, x, out=o8, workspace=ws), 2)
+    o8.zero_()
+    lg8.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(o8, ops.scl_decode(p8, x)), "SCL graph replay"
