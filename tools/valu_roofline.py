@@ -27,6 +27,7 @@ import re
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 import sys  # noqa: E402
 sys.path.insert(0, os.path.join(ROOT, "polar-code-pytorch-sionna_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
 KERNELS = {"sc": "pl_sc_static_f32", "scl": "scl_tree_kernel<8, 4, 0, false>", "scx": "pl_sc_static_f32"}
 KEYS = {"sc": "sc_k512_n1024_bs65536", "scl": "scl_k512_n1024_bs8192_L8", "scx": "sc_exact_k512_n1024_bs65536"}
 PINS = {"sc": "sc_k512_n1024_minsum", "scl": "scl_L8_n1024_minsum", "scx": None}  # scx: stale by source hash
@@ -85,8 +86,13 @@ def main():
         known_ns = sum(classes[c] * cal[CLASSES[c]] for c in classes)
         from polar_amd import build as _b
         keep = vj.get(KEYS[dec], {}).get("static")  # tools/isa_walk.py valu: kept across SQ refreshes
+        if PINS[dec]:
+            sha = pins[PINS[dec]]["sha"]
+        else:  # the exact-f kernel is not pinned: the built kernel's stream (tools/isa_walk.py)
+            import isa_walk
+            sha = isa_walk.isa_sha(isa_walk.kernel_asm(512, 1024, 1))
         vj[KEYS[dec]] = {
-            "kernel": KERNELS[dec], "isa_sha": pins[PINS[dec]]["sha"] if PINS[dec] else None,
+            "kernel": KERNELS[dec], "isa_sha": sha,
             "src_hash": _b.source_hash(), "dispatches": n, "waves_per_launch": waves,
             "valu_per_launch": total, "class_counts_per_launch": classes, "other_per_launch": other,
             "issue_ns_simd_per_launch": {"classified": known_ns, "other_lo": other * cal[OTHER[0]],
