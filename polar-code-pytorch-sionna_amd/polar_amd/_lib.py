@@ -270,8 +270,11 @@ class Plan:
         assert mask.shape == (n,)
         if int(list_size) == 1 and os.environ.get("PL_SC_SPECIALIZE") != "0" and \
                 not (flags & (PL_PLAN_GENERIC | PL_PLAN_CACHE_ONLY)):
-            # the library only loads cached code objects; compile out of process when missing
-            ensure_sc_kernel(n, mask, f_mode)
+            # the library only loads cached code objects; compile out of process when missing.
+            # Exact-f plans with llr_max > 43 (compared in fp32, as pl_plan_create does) run the
+            # full-range code object (jit.cpp attach_static)
+            wide = int(f_mode) == PL_F_EXACT and float(np.float32(llr_max)) > 43.0
+            ensure_sc_kernel(n, mask, int(f_mode) | (PL_F_WIDE_RANGE if wide else 0))
             flags |= PL_PLAN_CACHE_ONLY
         idx = device_index(device)
         self._h = ctypes.c_void_p()

@@ -297,3 +297,26 @@ def test_launch_graph_replays_bit_exact(pa):
     lg8.replay()
     torch.cuda.synchronize()
     assert torch.equal(o8, ops.scl_decode(p8, x)), "SCL graph replay"
+
+
+def test_sc_exact_wide_range_code_object(pa, tmp_path, monkeypatch):
+    """Exact-f plans get one code object per llr_max range (exactf.h PL_EXF_RANGE): llr_max 30 and
+    60 on the same code load different specialised kernels, the llr_max = 60 one compiled on demand
+    (out of process, into an empty cache); each equals the generic kernel (which tests the range
+    in every f) bit for bit."""
+    from polar_amd import _lib, ops
+    monkeypatch.setenv("PL_KERNEL_CACHE", str(tmp_path))
+    g = np.random.default_rng(5)
+    n = 64
+    fp = np.sort(g.permutation(n)[:28])
+    mask = pa.frozen_mask(fp, n)
+    x = torch.from_numpy((g.normal(0.0, 6.0, (1024, n))).astype(np.float32)).cuda()
+    paths = []
+    for lmax in (30.0, 60.0):
+        p = _lib.Plan(n, mask, 1, _lib.PL_F_EXACT, lmax)
+        kind, path = p.kernel()
+        assert kind == "specialized", (lmax, kind)
+        paths.append(path)
+        gen = _lib.Plan(n, mask, 1, _lib.PL_F_EXACT, lmax, flags=_lib.PL_PLAN_GENERIC)
+        assert torch.equal(ops.sc_decode(p, x), ops.sc_decode(gen, x)), lmax
+    assert paths[0] != paths[1], paths
