@@ -49,6 +49,7 @@ def parse():
                     help="distinct resident batches the steps cycle through (default 3 SC, 1 SCL)")
     ap.add_argument("--decoder", choices=["sc", "scl"], default="sc")
     ap.add_argument("--list-size", type=int, default=8)
+    ap.add_argument("--fast-scl", action="store_true", help="SCL: fast-SCL pruning (my_sn SCL_Dec's default)")
     ap.add_argument("--fmode", type=int, default=0, choices=[0, 1],
                     help="f of the decoder: 0 min-sum (x_run SC_Dec / SCL_Dec, the headline), 1 the exact boxplus f "
                          "(my_sn SC_Dec / SCL_Dec; profiling runs)")
@@ -231,15 +232,16 @@ def _time_launches(fn, steps, warmup, settle_ms, dev):
     return e0.elapsed_time(e1) / steps
 
 
-def config_line(decoder, k, n, bs, L, ebno, dev, rank, steps, warmup, fmode=0):
+def config_line(decoder, k, n, bs, L, ebno, dev, rank, steps, warmup, fmode=0, fast=False):
     """One more BASELINE.json configuration on this GPU, measured after the headline's timed
     region: kernel ms per launch (HIP events over back-to-back launches on one resident batch),
     Mcodewords/s, info Gbit/s, BLER, and the HBM roofline of the launch (bs (4n + 4k) bytes).
-    fmode 1: the exact boxplus f (my_sn SC_Dec / SCL_Dec)."""
+    fmode 1: the exact boxplus f (my_sn SC_Dec / SCL_Dec); fast: fast-SCL pruning (my_sn SCL_Dec's
+    default, PL_PLAN_FAST_SCL)."""
     import polar_amd
     from polar_amd import _lib, channel, ops
     fp = polar_amd.reference_frozen_pos(k, n)
-    plan = _lib.Plan(n, polar_amd.frozen_mask(fp, n), L, fmode, device=dev)
+    plan = _lib.Plan(n, polar_amd.frozen_mask(fp, n), L, fmode, flags=_lib.PL_PLAN_FAST_SCL if fast else 0, device=dev)
     gen = torch.Generator(device=dev).manual_seed(1042 + rank)
     model = channel.System_AWGN_model(n, k, channel.GpuEncoder(fp, n), None, device=dev, generator=gen)
     with torch.no_grad():
@@ -256,7 +258,7 @@ def config_line(decoder, k, n, bs, L, ebno, dev, rank, steps, warmup, fmode=0):
     nbytes = bs * (4 * n + 4 * k)
     ach = nbytes / (ms * 1e-3) / 1e9
     res = {"workload": f"{'SCL' if L > 1 else 'SC'} decode (k={k}, n={n}), bs={bs}" + (f", L={L}" if L > 1 else "")
-           + (", exact boxplus f (my_sn)" if fmode == 1 else ""),
+           + (", exact boxplus f (my_sn)" if fmode == 1 else "") + (", fast-SCL" if fast else ""),
            "kernel": plan.kernel()[0], "kernel_ms": round(ms, 5), "steps": steps,
            "mcw_s": round(bs / ms / 1e3, 3), "info_gbit_s": round(bs * k / ms / 1e6, 4),
            "dtype": "f64" if L > 1 else "f32", "bler": round(nerr / bs, 6),
@@ -466,7 +468,7 @@ def main():
     fp = polar_amd.reference_frozen_pos(k, n)
     mask = polar_amd.frozen_mask(fp, n)
     L = a.list_size if a.decoder == "scl" else 1
-    plan = _lib.Plan(n, mask, L, a.fmode, device=dev)
+    plan = _lib.Plan(n, mask, L, a.fmode, flags=_lib.PL_PLAN_FAST_SCL if (a.fast_scl and L > 1) else 0, device=dev)
     gen = torch.Generator(device=dev).manual_seed(42 + rank)
     model = channel.System_AWGN_model(n, k, channel.GpuEncoder(fp, n), None, device=dev, generator=gen)
     R = max(1, a.buffers)
@@ -530,7 +532,8 @@ def main():
     value = total_cw / wall / 1e6
     bytes_per_launch = bs * (4 * n + 4 * k)
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-    tag = f"{a.decoder}{'_exact' if a.fmode == 1 else ''}_k{k}_n{n}_bs{bs}" + (f"_L{L}" if L > 1 else "")
+    tag = (f"{a.decoder}{'_exact' if a.fmode == 1 else ''}{'_fast' if (a.fast_scl and L > 1) else ''}_k{k}_n{n}_bs{bs}"
+           + (f"_L{L}" if L > 1 else ""))
     sim_it = None
     if a.decoder == "sc" and a.fmode == 0 and not a.no_sim_iteration:
         sim_it = sim_iteration(plan, fp, k, n, bs, a.ebno, dev)
@@ -553,7 +556,12 @@ def main():
         rv = valu_roofline("sc_exact_k512_n1024_bs65536", cx["kernel_ms"])
         if rv is not None:
             cx["roofline_valu"] = rv
-        configs = {"configs_1": c1, "configs_3": c3, "mysn_sc_exact": cx}
+        # my_sn SCL_Dec's default (exact boxplus f + fast-SCL; also Polar5GDecoder's list decoder)
+        cs, _, _, _, _ = config_line("scl", 512, 1024, 8192, 8, a.ebno, dev, rank, 10, 2, fmode=1, fast=True)
+        rv = valu_roofline("scl_exact_fast_k512_n1024_bs8192_L8", cs["kernel_ms"])
+        if rv is not None:
+            cs["roofline_valu"] = rv
+        configs = {"configs_1": c1, "configs_3": c3, "mysn_sc_exact": cx, "mysn_scl": cs}
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.fmode == 0:
         cpu = cpu_baseline(llr.cpu().numpy(), fp.numpy(), k, n, a.decoder, L, a.cpu_seconds)

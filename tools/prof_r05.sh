@@ -6,7 +6,8 @@
 #  2. --pmc passes, each its own run: FETCH_SIZE and WRITE_SIZE of the SC headline kernel and of
 #     the SCL bench kernel (its private-memory VCache traffic);
 #  3. SQ passes (VALU class counts, waits) of the exact-f SC kernel (my_sn SC_Dec at (512,1024)),
-#     the min-sum SC kernel and the SCL kernel.
+#     the min-sum SC kernel, the SCL kernel and my_sn SCL_Dec's default (exact f + fast-SCL).
+# SQ_ONLY=1 runs step 3 only, SQ_DECS="..." picks its decoders.
 # Every step runs under its own timeout; the first failure ends the script.
 set -eo pipefail
 TAG=${1:?usage: prof_r05.sh TAG}
@@ -15,6 +16,7 @@ O=$R/gpurun_out
 cd /tmp && export TMPDIR=/tmp
 T=/tmp/${TAG}_prof
 B="--no-cpu-baseline --no-sim-iteration --no-configs --settle-ms 0"
+if [ -z "$SQ_ONLY" ]; then  # SQ_ONLY=1: the SQ passes only (SQ_DECS picks the decoders)
 timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $T/bench -o bench -- python3 $R/bench.py > $O/${TAG}_bench_traced.json 2> $O/${TAG}_bench_traced.err
 KT=$(find $T/bench -name "*kernel_trace.csv" | head -1)
 cp $(find $T/bench -name "*kernel_stats.csv" | head -1) $O/${TAG}_bench_kernel_stats.csv
@@ -26,12 +28,14 @@ for dec in sc scl; do
     cp $(find $T/pmc_${dec}_$c -name "*counter_collection.csv") $O/${TAG}_pmc_${dec}_$c.csv
   done
 done
+fi
 PA="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_CVT"
 PB="SQ_WAVES SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_INT64 SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"
 PC="SQ_WAVES SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_SMEM"
-for dec in scx sc scl; do
+for dec in ${SQ_DECS:-scx sc scl sclx}; do
   case $dec in
     scx) ARGS="--decoder sc --fmode 1" ;;
+    sclx) ARGS="--decoder scl --fmode 1 --fast-scl" ;;
     *) ARGS="--decoder $dec" ;;
   esac
   for p in A B C; do
@@ -43,6 +47,7 @@ for dec in scx sc scl; do
     [ $p = B ] && cp $(find $T/sq_${dec}_$p -name "*kernel_trace.csv") $O/${TAG}_sq_${dec}_B_trace.csv
   done
 done
+[ -n "$SQ_ONLY" ] && exit 0
 # the calibration kernels' clock: GRBM_GUI_ACTIVE cycles per dispatch against its trace duration
 timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU GRBM_GUI_ACTIVE --output-format csv -d $T/cal -o run -- $R/tools/micro/valu_cycles > $O/${TAG}_valu_cycles.txt 2> $O/${TAG}_valu_cycles.err
 cp $(find $T/cal -name "*counter_collection.csv") $O/${TAG}_valu_cycles_pmc.csv

@@ -28,9 +28,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 import sys  # noqa: E402
 sys.path.insert(0, os.path.join(ROOT, "polar-code-pytorch-sionna_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
-KERNELS = {"sc": "pl_sc_static_f32", "scl": "scl_tree_kernel<8, 4, 0, false>", "scx": "pl_sc_static_f32"}
-KEYS = {"sc": "sc_k512_n1024_bs65536", "scl": "scl_k512_n1024_bs8192_L8", "scx": "sc_exact_k512_n1024_bs65536"}
-PINS = {"sc": "sc_k512_n1024_minsum", "scl": "scl_L8_n1024_minsum", "scx": None}  # scx: stale by source hash
+KERNELS = {"sc": "pl_sc_static_f32", "scl": "scl_tree_kernel<8, 4, 0, false>", "scx": "pl_sc_static_f32",
+           "sclx": "scl_tree_kernel<8, 4, 1, true>"}
+KEYS = {"sc": "sc_k512_n1024_bs65536", "scl": "scl_k512_n1024_bs8192_L8", "scx": "sc_exact_k512_n1024_bs65536",
+        "sclx": "scl_exact_fast_k512_n1024_bs8192_L8"}
+# scx: the built exact-f kernel's stream (tools/isa_walk.py); sclx: stale by source hash
+PINS = {"sc": "sc_k512_n1024_minsum", "scl": "scl_L8_n1024_minsum", "scx": None, "sclx": None}
 # counter class -> calibration form(s) whose cost it carries
 CLASSES = {"SQ_INSTS_VALU_ADD_F32": "v_add_f32", "SQ_INSTS_VALU_MUL_F32": "v_mul_f32",
            "SQ_INSTS_VALU_FMA_F32": "v_fma_f32", "SQ_INSTS_VALU_TRANS_F32": "v_exp_f32",
@@ -88,9 +91,11 @@ def main():
         keep = vj.get(KEYS[dec], {}).get("static")  # tools/isa_walk.py valu: kept across SQ refreshes
         if PINS[dec]:
             sha = pins[PINS[dec]]["sha"]
-        else:  # the exact-f kernel is not pinned: the built kernel's stream (tools/isa_walk.py)
+        elif dec == "scx":  # the exact-f SC kernel is not pinned: the built kernel's stream (tools/isa_walk.py)
             import isa_walk
             sha = isa_walk.isa_sha(isa_walk.kernel_asm(512, 1024, 1))
+        else:
+            sha = None
         vj[KEYS[dec]] = {
             "kernel": KERNELS[dec], "isa_sha": sha,
             "src_hash": _b.source_hash(), "dispatches": n, "waves_per_launch": waves,
