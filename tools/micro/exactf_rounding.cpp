@@ -98,6 +98,7 @@ static uint32_t rnd() {
 }
 static double uni() { return rnd() / 4294967296.0; }
 
+#ifndef EXACTF_NO_MAIN  // tools/micro/exactf_exhaustive.cpp includes the forms above
 int main(int argc, char** argv) {
     const long N = argc > 1 ? atol(argv[1]) : 50000000;
     long be = 0, bl = 0, bl1 = 0, bf = 0, bs = 0;
@@ -125,3 +126,4 @@ int main(int argc, char** argv) {
            N, be, bl, bl1, bs, bf);
     return 0;
 }
+#endif
