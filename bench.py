@@ -302,7 +302,23 @@ def library_src_hash():
     return _lib.lib().pl_version().decode().split()[-1]
 
 
-def latency_bound(tag, kern_ms):
+def record_fresh(rec, tag, plan=None):
+    """Whether a profiles/ record describes the kernel this run executes: the content-addressed
+    code object name of a specialised SC kernel (changes exactly when its source does), the
+    pinned instruction stream (tests/golden/kernel_isa.json), the sources of the SCL subtree
+    kernel, or else the whole library's source hash."""
+    if rec.get("code_object") and plan is not None:
+        return os.path.basename(plan.kernel()[1]) == rec["code_object"]
+    pin = current_isa_sha(tag)
+    if pin:
+        return rec.get("isa_sha") == pin
+    if rec.get("kernel_src_hash"):
+        from polar_amd import build as _b
+        return rec["kernel_src_hash"] == _b.kernel_source_hash(_b.SCL_TREE_SOURCES)
+    return rec.get("src_hash") == library_src_hash()
+
+
+def latency_bound(tag, kern_ms, plan=None):
     """Independent critical-path bound of a batch that fills less than one wave per SIMD
     (profiles/latency.json, tools/isa_walk.py chain): the longest register-dependence chain of one
     wave's instruction stream, each edge weighted by the single-wave dependent latency
@@ -317,7 +333,7 @@ def latency_bound(tag, kern_ms):
         return None
     out = {"bound": "latency", "source": "profiles/latency.json", "chain_cycles": rec["chain_cycles"],
            "clock_ghz": rec["clock_ghz"], "latency_table": rec["latency_table"]}
-    if rec.get("src_hash") != library_src_hash() or not rec.get("clock_ghz"):
+    if not record_fresh(rec, tag, plan) or not rec.get("clock_ghz"):
         out.update({"stale": True, "frac": None})
         return out
     floor = rec["launch_floor_us"].get("256")
@@ -374,7 +390,7 @@ def current_isa_sha(tag):
         return None
 
 
-def valu_roofline(tag, kern_ms):
+def valu_roofline(tag, kern_ms, plan=None):
     """VALU-issue roofline of the kernel from its measured instruction mix: per launch, the SQ
     class counters (rocprofv3) times each class's issue cost (ns per wave-instruction per SIMD,
     calibrated by tools/micro/valu_cycles.hip at a settled clock), summed and spread over the
@@ -386,7 +402,7 @@ def valu_roofline(tag, kern_ms):
     v = valu_from_profiles(tag)
     if v and "static" in v:
         st = v["static"]
-        fresh = st.get("isa_sha") == current_isa_sha(tag) if current_isa_sha(tag) else st.get("src_hash") == library_src_hash()
+        fresh = record_fresh(st, tag, plan)
         out = {"bound": "valu_issue", "unit": "us of VALU issue per SIMD per launch", "kernel_ms": round(kern_ms, 5),
                "method": "per-mnemonic: the walked instruction stream (tools/isa_walk.py) x calibrated issue cost per "
                          "form (tools/micro/valu_cycles.hip); the residual against SQ_INSTS_VALU as a cost range",
@@ -411,8 +427,7 @@ def valu_roofline(tag, kern_ms):
     out = {"bound": "valu_issue", "unit": "us of VALU issue per SIMD per launch", "kernel_ms": round(kern_ms, 5),
            "valu_instr_per_launch": v["valu_per_launch"], "counter_files": v.get("source"),
            "isa_sha": v.get("isa_sha")}
-    pin = current_isa_sha(tag)
-    if (v.get("isa_sha") != pin) if pin else (v.get("src_hash") != library_src_hash()):
+    if not record_fresh(v, tag, plan):
         out.update({"stale": True, "frac": None, "frac_lo": None, "frac_hi": None})
         return out
     ns = v["issue_ns_simd_per_launch"]
@@ -542,23 +557,23 @@ def main():
         # BASELINE.json configs[1] (k=128, n=256, bs=4096, SC) and configs[3] (k=512, n=1024,
         # L=8, bs=8192, SCL) on this GPU, after the headline's timed region
         c1, f1, p1, l1, _ = config_line("sc", 128, 256, 4096, 1, a.ebno, dev, rank, 2000, 200)
-        c1["roofline_latency"] = latency_bound("sc_k128_n256", c1["kernel_ms"])
+        c1["roofline_latency"] = latency_bound("sc_k128_n256", c1["kernel_ms"], p1)
         # the same launches replayed from a captured HIP graph (the launch gap of a small batch)
         rl = c1["roofline_latency"]
         c1["graph"] = graph_line(f1, 200, dev, rl.get("chain_us") if rl and not rl.get("stale") else None)
         c1["single_wave"] = latency_roofline(p1, l1, 128, 256, 4096, c1["kernel_ms"], dev)
-        c3, _, _, _, _ = config_line("scl", 512, 1024, 8192, 8, a.ebno, dev, rank, 20, 3)
-        rv = valu_roofline("scl_k512_n1024_bs8192_L8", c3["kernel_ms"])
+        c3, _, p3, _, _ = config_line("scl", 512, 1024, 8192, 8, a.ebno, dev, rank, 20, 3)
+        rv = valu_roofline("scl_k512_n1024_bs8192_L8", c3["kernel_ms"], p3)
         if rv is not None:
             c3["roofline_valu"] = rv
         # my_sn SC_Dec (the library API's default decoder, exact boxplus f) at the headline shape
-        cx, _, _, _, _ = config_line("sc", 512, 1024, 65536, 1, a.ebno, dev, rank, 50, 10, fmode=1)
-        rv = valu_roofline("sc_exact_k512_n1024_bs65536", cx["kernel_ms"])
+        cx, _, px, _, _ = config_line("sc", 512, 1024, 65536, 1, a.ebno, dev, rank, 50, 10, fmode=1)
+        rv = valu_roofline("sc_exact_k512_n1024_bs65536", cx["kernel_ms"], px)
         if rv is not None:
             cx["roofline_valu"] = rv
         # my_sn SCL_Dec's default (exact boxplus f + fast-SCL; also Polar5GDecoder's list decoder)
-        cs, _, _, _, _ = config_line("scl", 512, 1024, 8192, 8, a.ebno, dev, rank, 10, 2, fmode=1, fast=True)
-        rv = valu_roofline("scl_exact_fast_k512_n1024_bs8192_L8", cs["kernel_ms"])
+        cs, _, ps_, _, _ = config_line("scl", 512, 1024, 8192, 8, a.ebno, dev, rank, 10, 2, fmode=1, fast=True)
+        rv = valu_roofline("scl_exact_fast_k512_n1024_bs8192_L8", cs["kernel_ms"], ps_)
         if rv is not None:
             cs["roofline_valu"] = rv
         configs = {"configs_1": c1, "configs_3": c3, "mysn_sc_exact": cx, "mysn_scl": cs}
@@ -594,7 +609,7 @@ def main():
             "cpu_baseline": cpu,
             "dist_backend": backend,
         }
-        rv = valu_roofline(tag, kern_ms)
+        rv = valu_roofline(tag, kern_ms, plan)
         if a.decoder == "scl" and rv is not None:
             # the list decoder is bound by VALU issue and leaf latency (0.6 % of HBM): its roofline is
             # the VALU one, the HBM figure stays next to it

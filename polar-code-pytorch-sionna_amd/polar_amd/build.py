@@ -42,16 +42,32 @@ def _needs(obj, src, deps):
     return any(os.path.getmtime(d) > t for d in [src] + deps)
 
 
-def source_hash():
-    """FNV-1a 64 over the library's sources (csrc/*, the C header) in name order: pl_version()
-    reports it, so a prebuilt library that travels without its sources can be matched to them."""
+def _fnv_files(paths):
     h = 0xcbf29ce484222325
-    files = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp", ".h")))
-    paths = [os.path.join(CSRC, f) for f in files] + [os.path.join(HERE, "..", "..", "include", "polar_mi355x.h")]
     for path in paths:
         for b in os.path.basename(path).encode() + b"\0" + open(path, "rb").read():
             h = ((h ^ b) * 0x100000001b3) & 0xFFFFFFFFFFFFFFFF
     return f"{h:016x}"
+
+
+HEADER = os.path.join(HERE, "..", "..", "include", "polar_mi355x.h")
+
+
+def source_hash():
+    """FNV-1a 64 over the library's sources (csrc/*, the C header) in name order: pl_version()
+    reports it, so a prebuilt library that travels without its sources can be matched to them."""
+    files = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".cpp", ".h")))
+    return _fnv_files([os.path.join(CSRC, f) for f in files] + [HEADER])
+
+
+# the sources the subtree SCL kernel is compiled from (profiles/valu.json records of its SQ passes
+# stay valid while these are unchanged, whatever else in csrc/ changes)
+SCL_TREE_SOURCES = ("scl_tree_kernel.hip", "softplus.h", "plan.h")
+
+
+def kernel_source_hash(files):
+    """FNV-1a 64 over the named csrc/ files and the C header, in the given order."""
+    return _fnv_files([os.path.join(CSRC, f) for f in files] + [HEADER])
 
 
 def _write_src_hash(obj_dir):

@@ -193,8 +193,11 @@ std::string static_source(int n, const uint8_t* frozen, int f_mode_in) {
     // Exact f: one code object per llr_max range (exactf.h PL_EXF_RANGE), so no f tests llr_max
     // and the lane-level f is inlined in the fast one (same-process A/B at (512,1024), bs = 65536,
     // profiles/r05f_sc_exact_ab_1024.txt: 0.9181 ms with the test in every f, 0.8618 without,
-    // 0.8126 inlined; (128,256) 0.1802 / 0.1723 / 0.1705 ms).
-    if (f_mode == PL_F_EXACT) o << (wide ? "#define PL_EXF_RANGE 2\n" : "#define PL_EXF_RANGE 1\n#define PL_SC_FLANE_INLINE 1\n");
+    // 0.8126 inlined; (128,256) 0.1802 / 0.1723 / 0.1705 ms).  Not inlined at n = 2048, whose
+    // inlined kernel takes ~3 minutes to compile (the critical path of the code-object pre-build).
+    if (f_mode == PL_F_EXACT)
+        o << (wide ? "#define PL_EXF_RANGE 2\n"
+                   : (log_n <= 10 ? "#define PL_EXF_RANGE 1\n#define PL_SC_FLANE_INLINE 1\n" : "#define PL_EXF_RANGE 1\n"));
     const int G = 1 << lg, NS = n >> lg;
     if (NS == 64) o << "#define PL_SC_SIM 1\n";  // the fused Monte-Carlo entry (sc_static.h OUT_SIM)
     std::string body = kStaticSrc;

@@ -387,8 +387,17 @@ def isa_sha(asm, kernel="pl_sc_static_f32"):
     return t.isa_summary(asm, lambda nm: nm == kernel)[kernel]["sha"]
 
 
+def code_object_name(k, n, fmode):
+    """Cache file name of the specialised SC kernel of the reference (k, n) code (content-addressed:
+    it changes exactly when the kernel's source does)."""
+    import polar_amd
+    from polar_amd import _lib
+    fp = polar_amd.reference_frozen_pos(k, n).numpy()
+    return _lib.sc_source(n, polar_amd.frozen_mask(fp, n), fmode)[1]
+
+
 def record_valu(asm, tag, cal_path, sq_valu_per_wave=None, waves_per_launch=None, codewords_per_wave=None,
-                normalise=False):
+                normalise=False, code_object=None):
     """profiles/valu.json[tag]["static"]: the walked stream's VALU per wave by mnemonic, each with
     its calibrated issue cost (tools/micro/valu_cycles.hip), and the residual against the SQ
     counter (instructions the walk does not see: rare fallbacks) carried as a cost range."""
@@ -423,7 +432,7 @@ def record_valu(asm, tag, cal_path, sq_valu_per_wave=None, waves_per_launch=None
     resid = (sq_valu_per_wave - walk_valu) if sq_valu_per_wave is not None else 0.0
     un = sum(unmapped.values())
     from polar_amd import build as _b
-    rec = {"isa_sha": isa_sha(asm), "src_hash": _b.source_hash(), "calibration": cal_path,
+    rec = {"isa_sha": isa_sha(asm), "src_hash": _b.source_hash(), "code_object": code_object, "calibration": cal_path,
            "clock_normalised": bool(f_dec), "kernel_clock_ghz": f_dec, "valu_per_wave_walk": walk_valu,
            "valu_per_wave_sq": sq_valu_per_wave, "residual_per_wave": round(resid, 1),
            "issue_ns_per_wave": {"mapped": round(mapped_ns, 1),
@@ -440,7 +449,7 @@ def record_valu(asm, tag, cal_path, sq_valu_per_wave=None, waves_per_launch=None
     return rec
 
 
-def record_chain(asm, tag, lat_path, kernel_ms=None):
+def record_chain(asm, tag, lat_path, kernel_ms=None, code_object=None):
     """profiles/latency.json[tag]: the walked stream's longest register-dependence chain (cycles,
     chain_latency.hip's per-form latencies) and the in-order single-wave estimate, in us at the
     measured s_memtime clock, plus the back-to-back launch floor."""
@@ -454,7 +463,8 @@ def record_chain(asm, tag, lat_path, kernel_ms=None):
     tr = walk(ins)
     longest, est = chain(ins, tr, lat)
     from polar_amd import build as _b
-    rec = {"isa_sha": isa_sha(asm), "src_hash": _b.source_hash(), "latency_table": lat_path, "instructions_per_wave": len(tr),
+    rec = {"isa_sha": isa_sha(asm), "src_hash": _b.source_hash(), "code_object": code_object, "latency_table": lat_path,
+           "instructions_per_wave": len(tr),
            "chain_cycles": round(longest, 1), "in_order_cycles": round(est, 1), "clock_ghz": clock,
            "chain_us": round(longest / clock / 1e3, 3) if clock else None,
            "in_order_us": round(est / clock / 1e3, 3) if clock else None,
@@ -499,11 +509,13 @@ def main():
         if sq is not None and vj[tag].get("isa_sha") not in (None, isa_sha(asm)):
             sq = None  # the SQ pass counted another instruction stream
         waves = vj.get(tag, {}).get("waves_per_launch") or (a.bs // a.cpw if a.cpw else None)
-        rec = record_valu(asm, tag, a.cal, sq, waves, a.cpw, a.clock_normalise)
+        rec = record_valu(asm, tag, a.cal, sq, waves, a.cpw, a.clock_normalise,
+                          None if a.asm else code_object_name(a.k, a.n, a.fm))
         print(json.dumps({k: rec[k] for k in ("valu_per_wave_walk", "valu_per_wave_sq", "issue_ns_per_wave", "unmapped")}))
         return
     if a.cmd == "chain":
-        rec = record_chain(asm, a.tag or f"sc_k{a.k}_n{a.n}", a.lat)
+        rec = record_chain(asm, a.tag or f"sc_k{a.k}_n{a.n}", a.lat,
+                           code_object=None if a.asm else code_object_name(a.k, a.n, a.fm))
         print(json.dumps({k: v for k, v in rec.items() if k != "latency_table"}))
 
 

@@ -88,16 +88,20 @@ def main():
         other = total - sum(classes.values())
         known_ns = sum(classes[c] * cal[CLASSES[c]] for c in classes)
         from polar_amd import build as _b
+        import isa_walk
         keep = vj.get(KEYS[dec], {}).get("static")  # tools/isa_walk.py valu: kept across SQ refreshes
         if PINS[dec]:
             sha = pins[PINS[dec]]["sha"]
         elif dec == "scx":  # the exact-f SC kernel is not pinned: the built kernel's stream (tools/isa_walk.py)
-            import isa_walk
             sha = isa_walk.isa_sha(isa_walk.kernel_asm(512, 1024, 1))
         else:
             sha = None
         vj[KEYS[dec]] = {
             "kernel": KERNELS[dec], "isa_sha": sha,
+            # freshness keys bench.py checks: the exact-f SC code object's content-addressed name;
+            # the sources of the SCL subtree kernel
+            "code_object": isa_walk.code_object_name(512, 1024, 1) if dec == "scx" else None,
+            "kernel_src_hash": _b.kernel_source_hash(_b.SCL_TREE_SOURCES) if dec in ("scl", "sclx") else None,
             "src_hash": _b.source_hash(), "dispatches": n, "waves_per_launch": waves,
             "valu_per_launch": total, "class_counts_per_launch": classes, "other_per_launch": other,
             "issue_ns_simd_per_launch": {"classified": known_ns, "other_lo": other * cal[OTHER[0]],
