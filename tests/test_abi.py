@@ -147,6 +147,30 @@ def test_sc_source_and_cache_name():
     assert _lib.sc_source(1024, m2, 0)[1] != name
 
 
+def test_exact_f_code_objects_per_llr_max_range():
+    """Exact-f codes have one source per llr_max range (exactf.h PL_EXF_RANGE): <= 43 the fast
+    forms with the lane-level f inlined (n <= 1024), > 43 (f_mode | PL_F_WIDE_RANGE) the full-range
+    forms; the two are different cache objects; the flag is refused for min-sum codes."""
+    import ctypes
+
+    import polar_amd
+    from polar_amd import _lib
+    m = polar_amd.frozen_mask(polar_amd.reference_frozen_pos(512, 1024).numpy(), 1024)
+    fast, nf = _lib.sc_source(1024, m, _lib.PL_F_EXACT)
+    wide, nw = _lib.sc_source(1024, m, _lib.PL_F_EXACT | _lib.PL_F_WIDE_RANGE)
+    assert "#define PL_EXF_RANGE 1" in fast and "#define PL_SC_FLANE_INLINE 1" in fast
+    assert "#define PL_EXF_RANGE 2" in wide and "PL_SC_FLANE_INLINE 1" not in wide
+    assert nf != nw
+    m2 = polar_amd.frozen_mask(polar_amd.reference_frozen_pos(1024, 2048).numpy(), 2048)
+    src2, _ = _lib.sc_source(2048, m2, _lib.PL_F_EXACT)
+    assert "#define PL_EXF_RANGE 1" in src2 and "PL_SC_FLANE_INLINE 1" not in src2  # n = 2048: out of line
+    size = ctypes.c_size_t()
+    name = ctypes.create_string_buffer(64)
+    rc = _lib.lib().pl_sc_source(1024, m.ctypes.data_as(ctypes.c_void_p), _lib.PL_F_MINSUM | _lib.PL_F_WIDE_RANGE,
+                                 None, 0, ctypes.byref(size), name, 64)
+    assert rc == _lib.PL_EINVAL
+
+
 def test_prebuilt_kernels_cover_the_reference_codes():
     """build() pre-compiles (hipcc --genco) every code the reference, the bench and the GPU tests
     use, so nothing compiles on the GPU box."""
