@@ -415,6 +415,53 @@ __device__ __forceinline__ int rank16_split(double cv) {
 }
 #undef PL_RANK_ROT_A
 #undef PL_RANK_ROT_B
+// Rank from the high words alone, checked.  Metrics are non-negative doubles, so when the 16
+// candidates of a row have 16 different high words (sign, exponent, top 20 mantissa bits) the high
+// words order them exactly like the full values, and the count of smaller high words is the rank:
+// per rotation one DPP subtract (its borrow = the rotated high word is smaller) and one carry add,
+// 2 VALU instead of 3-5 plus SALU tie masks.  Equal high words (the dead paths' equal metrics of
+// the first information bits, metrics within ~2^-20 of each other) give two lanes the same count;
+// the ranks of a row then do not cover 0..15, which the OR of 1 << rank over the row shows
+// (4 DPP ORs), and the wave takes the full 64-bit stable rank instead -- the same ranks either way.
+// Same-process A/B at (512,1024), L = 8, bs = 8192: 0.848 -> 0.803 ms on N(1, 2.5^2) LLRs
+// (profiles/r05s_scl_rankhi_ab.txt), 0.850 -> 0.837 ms on the bench's AWGN LLRs at 2 dB
+// (r05u_scl_rankhi_ab_awgn.txt), bit-identical.  There the check fails more often (the CPU oracle:
+// 3.5 % of a codeword's information leaves have equal high words among the candidates, 1.8 % exactly
+// equal metrics -- LLRs of exactly 0 -- so ~13 % of the 4-codeword waves), and the branch itself
+// costs: with a trivial fallback body 0.807 ms, without the branch 0.767 ms (diagnostics
+// PL_SCL_DIAG_RANK_FB, r05w_scl_fb2_ab.txt).  The fp32 rounding of the metric as the key (ties
+// 8x rarer) measured 0.844 ms; issuing the push before the check 0.872 ms (r05v, r05w).
+#ifndef PL_SCL_RANK_HI
+#define PL_SCL_RANK_HI 1
+#endif
+#define PL_RANK_ROT_H(r)                                                                     \
+    "v_sub_co_u32_dpp %1, vcc, %3, %3 row_ror:" #r " row_mask:0xf bank_mask:0xf\n\t" \
+    "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n\t"
+__device__ __forceinline__ int rank16_hi(double cv, bool& ok) {
+    const int hi = (int)(__double_as_longlong(cv) >> 32);
+    int rk, tmp, cover;
+    asm volatile(
+        "s_nop 1\n\t"  // the DPP source was just written by a VALU
+        "v_mov_b32 %0, 0\n\t"
+        PL_RANK_ROT_H(1) PL_RANK_ROT_H(2) PL_RANK_ROT_H(3) PL_RANK_ROT_H(4) PL_RANK_ROT_H(5)
+        PL_RANK_ROT_H(6) PL_RANK_ROT_H(7) PL_RANK_ROT_H(8) PL_RANK_ROT_H(9) PL_RANK_ROT_H(10)
+        PL_RANK_ROT_H(11) PL_RANK_ROT_H(12) PL_RANK_ROT_H(13) PL_RANK_ROT_H(14) PL_RANK_ROT_H(15)
+        "v_lshlrev_b32 %2, %0, 1\n\t"
+        "s_nop 1\n\t"
+        "v_or_b32_dpp %2, %2, %2 row_ror:1 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_or_b32_dpp %2, %2, %2 row_ror:2 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_or_b32_dpp %2, %2, %2 row_ror:4 row_mask:0xf bank_mask:0xf\n\t"
+        "s_nop 1\n\t"
+        "v_or_b32_dpp %2, %2, %2 row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
+        : "=&v"(rk), "=&v"(tmp), "=&v"(cover)
+        : "v"(hi)
+        : "vcc");
+    ok = cover == 0xffff;
+    return rk;
+}
+#undef PL_RANK_ROT_H
 #endif
 
 // ---- X2 helpers (two rows per codeword) ---------------------------------------------------
@@ -1685,6 +1732,22 @@ __device__ __forceinline__ int rank_2l(double cv, int gl, int lane) {
             const double v = readlane_d(cv, c);
             rk += (v < cv || (v == cv && c < lane)) ? 1 : 0;
         }
+#if PL_SCL_RANK_SUBB && PL_SCL_RANK_HI
+    } else if constexpr (GW == 16) {
+        bool ok;
+        rk = rank16_hi(cv, ok);
+#if PL_DEV && defined(PL_SCL_DIAG_RANK_FB)  // timing diagnostic: 0 never / 1 always take the full rank
+        if (PL_SCL_DIAG_RANK_FB < 2) ok = PL_SCL_DIAG_RANK_FB == 0;
+#endif
+        if (__builtin_amdgcn_ballot_w64(!ok) != 0) {  // equal high words in some row: the full rank
+#if PL_DEV && defined(PL_SCL_DIAG_RANK_FB) && PL_SCL_DIAG_RANK_FB == 2  // the branch with a trivial body
+            rk = gl;
+#else
+            if constexpr (FM == 0 && PL_SCL_RANK_SPLIT) rk = rank16_split(cv);
+            else rk = rank16_subb(cv);
+#endif
+        }
+#endif
     } else if constexpr (GW == 16 && FM == 0 && PL_SCL_RANK_SUBB && PL_SCL_RANK_SPLIT) {
         rk = rank16_split(cv);  // min-sum kernels only: its 14 mask SGPRs spill the exact-f ones
     } else {

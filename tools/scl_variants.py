@@ -52,6 +52,13 @@ def time_all(n=1024, k=512, bs=8192, reps=5, rounds=2):
     mask = np.ascontiguousarray(polar_amd.frozen_mask(fp, n), dtype=np.uint8)
     g = torch.Generator(device="cuda").manual_seed(5)
     llr = torch.randn((bs, n), device="cuda", generator=g) * 2.5 + 1.0
+    if os.environ.get("SCL_INPUT") == "awgn":  # the bench's input: AWGN LLRs at Eb/N0 = 2 dB
+        from polar_amd import channel
+        model = channel.System_AWGN_model(n, k, channel.GpuEncoder(torch.as_tensor(fp), n), None, device="cuda",
+                                          generator=g)
+        with torch.no_grad():
+            _, _, llr = model.llrs(bs, torch.tensor(2.0))
+        llr = llr.contiguous()
     ref = None
     handles = []
     for name, path in libs:
