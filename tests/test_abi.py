@@ -319,3 +319,29 @@ def test_bench_valu_roofline_from_committed_counters():
         assert rv["stale"] is True and rv["frac"] is None
     finally:
         bench.current_isa_sha = orig
+
+
+def test_bench_records_keyed_to_their_kernels():
+    """bench.py record_fresh: a record that names a specialised SC code object is current exactly
+    while the plan loads that object; the SCL subtree records follow the hash of their own sources;
+    the committed exact-f SC, SCL and my_sn SCL records are current for the built tree."""
+    import importlib.util
+    import json
+    import types
+    spec = importlib.util.spec_from_file_location("bench_mod2", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    from polar_amd import _lib
+    import polar_amd
+    m = polar_amd.frozen_mask(polar_amd.reference_frozen_pos(512, 1024).numpy(), 1024)
+    name = _lib.sc_source(1024, m, _lib.PL_F_EXACT)[1]
+    plan = types.SimpleNamespace(kernel=lambda: ("specialized", "/somewhere/kcache/" + name))
+    other = types.SimpleNamespace(kernel=lambda: ("specialized", "/somewhere/kcache/sc_0000000000000000.co"))
+    rec = {"code_object": name}
+    assert bench.record_fresh(rec, "sc_exact_k512_n1024_bs65536", plan)
+    assert not bench.record_fresh(rec, "sc_exact_k512_n1024_bs65536", other)
+    vj = json.load(open(os.path.join(ROOT, "profiles", "valu.json")))
+    assert bench.record_fresh(vj["sc_exact_k512_n1024_bs65536"]["static"], "sc_exact_k512_n1024_bs65536", plan)
+    for tag in ("scl_k512_n1024_bs8192_L8", "scl_exact_fast_k512_n1024_bs8192_L8"):
+        assert bench.record_fresh(vj[tag], tag), tag
+    assert not bench.record_fresh({"kernel_src_hash": "0" * 16}, "scl_exact_fast_k512_n1024_bs8192_L8")
