@@ -509,11 +509,20 @@ __device__ __forceinline__ double exp_d(float xf) {
 __device__ __forceinline__ float exp_cr(float xf) { return (float)exp_d(xf); }
 // fp32 e^(fl(xc + yc)) from the fp64 e^xc, e^yc: e^xc e^yc e^d, d = fl(xc + yc) - (xc + yc), which
 // Fast2Sum gives exactly in fp32 ((s - a) - b with |a| >= |b|)
+#ifndef PL_EXF_TWOSUM
+#define PL_EXF_TWOSUM 1  // d by the branch-free TwoSum (5 adds) instead of the ordered Fast2Sum (compare, 2 selects, 2 subs): A/B 0.8155 -> 0.8089 ms, bit-identical (profiles/r05zz_sc_exact_twosum_ab.txt)
+#endif
 __device__ __forceinline__ float exp_sum(double ex, double ey, float xc, float yc) {
     const float s = xc + yc;
+#if PL_EXF_TWOSUM
+    // TwoSum: e = (xc + yc) - s exactly, d = -e; the same exact value as the ordered form
+    const float bb = s - xc;
+    const double d = -(double)((xc - (s - bb)) + (yc - bb));
+#else
     const bool sw = __builtin_fabsf(yc) > __builtin_fabsf(xc);
     const float a = sw ? yc : xc, b = sw ? xc : yc;
     const double d = (double)((s - a) - b);
+#endif
     return (float)(ex * ey * __builtin_fma(d, __builtin_fma(d, 0.5, 1.0), 1.0));
 }
 

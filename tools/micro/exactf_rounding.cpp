@@ -57,13 +57,14 @@ static float exp_ref(float x) { return (float)expl((long double)x); }
 static float log_ref(float x) { return (float)logl((long double)x); }
 
 // exactf.h exp_sum: fp32 e^(fl(xc + yc)) from the fp64 e^xc, e^yc and the Fast2Sum error d
-static float exp_sum(double ex, double ey, float xc, float yc) {
+static float exp_sum(double ex, double ey, float xc, float yc) {  // PL_EXF_TWOSUM: the exact error by TwoSum
     volatile float s = xc + yc;
-    const bool sw = fabsf(yc) > fabsf(xc);
-    const float a = sw ? yc : xc, b = sw ? xc : yc;
-    volatile float t = s - a;
-    volatile float dd = t - b;
-    const double d = (double)dd;
+    volatile float bb = s - xc;
+    volatile float t = s - bb;
+    volatile float e1 = xc - t;
+    volatile float e2 = yc - bb;
+    volatile float e = e1 + e2;
+    const double d = -(double)e;
     return (float)(ex * ey * fma(d, fma(d, 0.5, 1.0), 1.0));
 }
 // exactf.h f_exact (PL_EXF_LEAN)
