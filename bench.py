@@ -232,6 +232,31 @@ def _time_launches(fn, steps, warmup, settle_ms, dev):
     return e0.elapsed_time(e1) / steps
 
 
+def launch_stats(fn, launches, dev):
+    """Per-launch kernel times of `launches` more back-to-back calls, each bracketed by its own pair
+    of HIP events on the launch stream (after the mean's timed region, so that one is unperturbed):
+    min and median ms, next to the mean the timed region gives."""
+    stream = torch.cuda.current_stream(dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(launches + 1)]
+    ev[0].record(stream)
+    for i in range(launches):
+        fn()
+        ev[i + 1].record(stream)
+    torch.cuda.synchronize(dev)
+    t = sorted(ev[i].elapsed_time(ev[i + 1]) for i in range(launches))
+    return {"min_ms": round(t[0], 5), "median_ms": round(t[len(t) // 2], 5), "launches": launches}
+
+
+def clock_ghz(dev):
+    """The shader clock of one CU now (pl_clock_probe, on the decode stream: it runs right after the
+    launches queued before it), or None if the probe is unavailable."""
+    try:
+        from polar_amd import ops
+        return round(ops.shader_clock_ghz(dev), 4)
+    except Exception:
+        return None
+
+
 def config_line(decoder, k, n, bs, L, ebno, dev, rank, steps, warmup, fmode=0, fast=False):
     """One more BASELINE.json configuration on this GPU, measured after the headline's timed
     region: kernel ms per launch (HIP events over back-to-back launches on one resident batch),
@@ -254,12 +279,14 @@ def config_line(decoder, k, n, bs, L, ebno, dev, rank, steps, warmup, fmode=0, f
     else:
         fn = lambda: ops.sc_decode(plan, llr, out=out)  # noqa: E731
     ms = _time_launches(fn, steps, warmup, 50.0, dev)
+    ls = launch_stats(fn, min(steps, 50), dev)
     nerr = int(torch.any(out != bits, dim=-1).sum().item())
     nbytes = bs * (4 * n + 4 * k)
     ach = nbytes / (ms * 1e-3) / 1e9
     res = {"workload": f"{'SCL' if L > 1 else 'SC'} decode (k={k}, n={n}), bs={bs}" + (f", L={L}" if L > 1 else "")
            + (", exact boxplus f (my_sn)" if fmode == 1 else "") + (", fast-SCL" if fast else ""),
            "kernel": plan.kernel()[0], "kernel_ms": round(ms, 5), "steps": steps,
+           "kernel_min_ms": ls["min_ms"], "kernel_median_ms": ls["median_ms"],
            "mcw_s": round(bs / ms / 1e3, 3), "info_gbit_s": round(bs * k / ms / 1e6, 4),
            "dtype": "f64" if L > 1 else "f32", "bler": round(nerr / bs, 6),
            "roofline_hbm": {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -345,24 +372,6 @@ def latency_bound(tag, kern_ms, plan=None):
     return out
 
 
-def latency_roofline(plan, llr, k, n, bs, ms_full, dev, steps=400):
-    """Latency bound of a batch that fills less than one wave per SIMD: the same launch with one
-    wave of codewords (64 / G of them, G = lanes per codeword of the specialised min-sum kernel:
-    n/64 for n = 256 ... 1024, else max(1, n/128)) -- the dependent chain of one wave on an idle
-    chip, launch included -- against the full batch's launch time.  frac = single-wave time / full
-    time (1.0 = the batch costs no more than its critical path)."""
-    from polar_amd import ops
-    g = n // 64 if 256 <= n <= 1024 else max(1, n // 128)
-    cpw = 64 // g
-    one = llr[:cpw].contiguous()
-    out1 = torch.empty((cpw, k), dtype=torch.float32, device=dev)
-    t1 = _time_launches(lambda: ops.sc_decode(plan, one, out=out1), steps, 20, 20.0, dev)
-    return {"bound": "latency", "single_wave_ms": round(t1, 5), "codewords_per_wave": cpw,
-            "waves": -(-bs // cpw), "achieved_ms": round(ms_full, 5), "frac": round(t1 / ms_full, 4),
-            "note": "one wave of codewords per launch (its dependent chain, on an idle chip) vs the whole "
-                    "batch; the batch fills fewer waves than the chip's 1024 SIMDs"}
-
-
 def plan_mask(fp, n):
     import polar_amd
     return polar_amd.frozen_mask(fp, n)
@@ -444,15 +453,20 @@ def valu_roofline(tag, kern_ms, plan=None):
     return out
 
 
-def traffic_from_profiles(tag):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if one exists for this shape."""
+def traffic_from_profiles(tag, plan=None):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (profiles/traffic.json), if one
+    exists for this shape and was measured on the kernel this run executes (its pinned instruction
+    stream or code object, when the record names one); else None."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     if not os.path.exists(path):
         return None
     try:
-        return json.load(open(path)).get(tag, {}).get("hbm_bytes_per_launch")
+        rec = json.load(open(path)).get(tag, {})
     except Exception:
         return None
+    if (rec.get("isa_sha") or rec.get("code_object")) and not record_fresh(rec, tag, plan):
+        return None
+    return rec.get("hbm_bytes_per_launch")
 
 
 def main():
@@ -516,6 +530,7 @@ def main():
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize(dev)
+    clk_before = clock_ghz(dev)  # the shader clock just before the timed region (after the warmup)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -534,6 +549,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     kern_ms = e0.elapsed_time(e1) / a.steps
+    clk_after = clock_ghz(dev)  # ... and right after its last launch
+    kstats = launch_stats(step, min(a.steps, 200), dev)
 
     cdev = dev if backend == "nccl" else torch.device("cpu")  # RCCL reduces device tensors, gloo host ones
     nerr = sum(int(torch.any(o != b, dim=-1).sum().item()) for o, b in zip(outs, bitss))
@@ -556,13 +573,14 @@ def main():
     if a.decoder == "sc" and a.fmode == 0 and not a.no_configs and (k, n, bs) == (512, 1024, 65536):
         # BASELINE.json configs[1] (k=128, n=256, bs=4096, SC) and configs[3] (k=512, n=1024,
         # L=8, bs=8192, SCL) on this GPU, after the headline's timed region
-        c1, f1, p1, l1, _ = config_line("sc", 128, 256, 4096, 1, a.ebno, dev, rank, 2000, 200)
+        c1, f1, p1, _, _ = config_line("sc", 128, 256, 4096, 1, a.ebno, dev, rank, 2000, 200)
         c1["roofline_latency"] = latency_bound("sc_k128_n256", c1["kernel_ms"], p1)
         # the same launches replayed from a captured HIP graph (the launch gap of a small batch)
         rl = c1["roofline_latency"]
         c1["graph"] = graph_line(f1, 200, dev, rl.get("chain_us") if rl and not rl.get("stale") else None)
-        c1["single_wave"] = latency_roofline(p1, l1, 128, 256, 4096, c1["kernel_ms"], dev)
         c3, _, p3, _, _ = config_line("scl", 512, 1024, 8192, 8, a.ebno, dev, rank, 20, 3)
+        # the HBM bytes the SCL launch moves (its lane-private virtual-node cache)
+        c3["roofline_hbm"]["traffic"] = traffic_from_profiles("scl_k512_n1024_bs8192_L8", p3)
         rv = valu_roofline("scl_k512_n1024_bs8192_L8", c3["kernel_ms"], p3)
         if rv is not None:
             c3["roofline_valu"] = rv
@@ -573,6 +591,7 @@ def main():
             cx["roofline_valu"] = rv
         # my_sn SCL_Dec's default (exact boxplus f + fast-SCL; also Polar5GDecoder's list decoder)
         cs, _, ps_, _, _ = config_line("scl", 512, 1024, 8192, 8, a.ebno, dev, rank, 10, 2, fmode=1, fast=True)
+        cs["roofline_hbm"]["traffic"] = traffic_from_profiles("scl_exact_fast_k512_n1024_bs8192_L8", ps_)
         rv = valu_roofline("scl_exact_fast_k512_n1024_bs8192_L8", cs["kernel_ms"], ps_)
         if rv is not None:
             cs["roofline_valu"] = rv
@@ -604,8 +623,15 @@ def main():
             "bler": round(float(blk[0].item()) / float(blk[1].item()), 6),
             "bler_reference_at_ebno": REF_BLER_2DB if (a.decoder == "sc" and k == 512 and n == 1024 and a.ebno == 2.0) else None,
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic_from_profiles(tag),
-                         "kernel_ms": round(kern_ms, 5), "algorithmic_bytes_per_launch": bytes_per_launch},
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic_from_profiles(tag, plan),
+                         "kernel_ms": round(kern_ms, 5), "kernel_min_ms": kstats["min_ms"],
+                         "kernel_median_ms": kstats["median_ms"], "algorithmic_bytes_per_launch": bytes_per_launch},
+            "kernel_ms_stats": dict(kstats, mean_ms=round(kern_ms, 5),
+                                    note="mean: the timed region's HIP events; min / median: one event pair per "
+                                         "launch over that many more launches after it"),
+            "clock_ghz": {"before": clk_before, "after": clk_after,
+                          "method": "pl_clock_probe: one wave's s_memtime cycles over s_memrealtime's 100 MHz ticks, "
+                                    "launched on the decode stream right before and right after the timed region"},
             "cpu_baseline": cpu,
             "dist_backend": backend,
         }

@@ -210,6 +210,13 @@ int pl_sc_sim_count(const pl_plan* plan, uint64_t seed, uint64_t iteration, int6
                     int64_t* counts, void* workspace, size_t ws_bytes, float* llr_dump, float* u_dump,
                     void* hip_stream);
 
+/* pl_clock_probe: diagnostics, not on the reference's path.  One wave runs iters dependent VALU adds
+ * and writes ticks[0] = s_memtime cycles (shader clock), ticks[1] = s_memrealtime ticks (100 MHz)
+ * and ticks[2] (the chain's result) to the DEVICE buffer ticks[3]; clock GHz = 0.1 * ticks[0] /
+ * ticks[1].  bench.py reads the clock around its timed region with it (DVFS moves the MI355X clock
+ * with load and from box to box). */
+int pl_clock_probe(uint64_t* ticks, int32_t iters, void* hip_stream);
+
 const char* pl_last_error_string(void);
 /* "polar_mi355x <version> (gfx950) src <16 hex digits>": the FNV-1a hash of the sources the library was
  * built from (polar_amd/build.py source_hash()). */

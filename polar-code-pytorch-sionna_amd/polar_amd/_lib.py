@@ -61,13 +61,14 @@ def _declare(L):
     L.pl_sc_decode_count.argtypes = [P, P, i64, P, P, P, ctypes.c_size_t, P]
     L.pl_sc_sim_count.argtypes = [P, ctypes.c_uint64, ctypes.c_uint64, i64, i64, ctypes.c_float, P, P,
                                   ctypes.c_size_t, P, P, P]
+    L.pl_clock_probe.argtypes = [P, i32, P]
     L.pl_last_error_string.restype = ctypes.c_char_p
     L.pl_version.restype = ctypes.c_char_p
     for f in (L.pl_plan_create, L.pl_plan_destroy, L.pl_plan_info, L.pl_plan_device, L.pl_sc_decode, L.pl_scl_decode,
               L.pl_polar_encode, L.pl_plan_kernel, L.pl_sc_specialize, L.pl_sc_source, L.pl_plan_set_crc,
               L.pl_crc_attach, L.pl_crc_check,
               L.pl_gather_rows, L.pl_rate_recover, L.pl_awgn_qpsk_llr, L.pl_count_errors,
-              L.pl_awgn_qpsk_llr_bits, L.pl_sc_decode_count, L.pl_sc_sim_count):
+              L.pl_awgn_qpsk_llr_bits, L.pl_sc_decode_count, L.pl_sc_sim_count, L.pl_clock_probe):
         f.restype = ctypes.c_int
     return L
 
@@ -103,7 +104,8 @@ EXPORTED_SYMBOLS = ("pl_plan_create", "pl_plan_destroy", "pl_plan_info", "pl_pla
                     "pl_plan_kernel", "pl_sc_specialize", "pl_sc_source", "pl_plan_set_crc", "pl_crc_attach",
                     "pl_crc_check", "pl_gather_rows",
                     "pl_rate_recover", "pl_awgn_qpsk_llr", "pl_count_errors", "pl_awgn_qpsk_llr_bits",
-                    "pl_sc_count_workspace_size", "pl_sc_decode_count", "pl_sc_sim_count", "pl_last_error_string", "pl_version")
+                    "pl_sc_count_workspace_size", "pl_sc_decode_count", "pl_sc_sim_count", "pl_clock_probe",
+                    "pl_last_error_string", "pl_version")
 
 
 def check(rc, what):

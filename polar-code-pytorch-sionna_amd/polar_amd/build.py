@@ -18,7 +18,7 @@ OBJ = os.path.join(HERE, "_obj")
 LIB = os.path.join(HERE, "libpolar_mi355x.so")
 KCACHE = os.path.join(HERE, "kcache")
 SOURCES = ["sc_kernel.hip", "scl_kernel.hip", "encode_kernel.hip", "ratematch_kernel.hip", "channel_kernel.hip",
-           "capi.cpp", "jit.cpp"]
+           "clock_kernel.hip", "capi.cpp", "jit.cpp"]
 # scl_tree_kernel.hip is compiled once per list size (its instantiations, in parallel) and once
 # for the launcher: (object name, source, defines)
 UNITS = [(s + ".o", s, []) for s in SOURCES] + \

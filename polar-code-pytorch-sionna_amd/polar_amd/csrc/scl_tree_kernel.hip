@@ -37,6 +37,7 @@
 #include <stdint.h>
 
 #include <type_traits>
+#include <utility>
 
 #include "../../../include/polar_mi355x.h"
 #include "plan.h"
@@ -52,7 +53,8 @@ namespace {
 #define PL_SCL_LOADGRP 0  // > 0: stage-R input read in groups of this many pairs (caps VGPRs)
 #endif
 #ifndef PL_SCL_UNROLL
-#define PL_SCL_UNROLL 1  // 1: the 2^R leaves of a lane-local subtree fully unrolled (A/B: 2.08 vs 2.27 ms)
+#define PL_SCL_UNROLL 1  // 1: the 2^R leaves of a lane-local subtree fully unrolled (A/B: 2.08 vs 2.27 ms; round 6,
+                        // constant leaf indices via unroll_leaves: 0.793 -> 0.744 ms, profiles/r06d_scl_unroll_ab.txt)
 #endif
 #ifndef PL_SCL_DIAG_NO_UPPER
 #define PL_SCL_DIAG_NO_UPPER 0
@@ -152,24 +154,6 @@ struct Prof {
 constexpr int R = PL_SCL_R;  // stage of the lane-local subtree
 constexpr int T = 1 << R;    // leaves per lane-local subtree (<= one partial-sum word)
 constexpr int SPS = 16;      // bytes per path of the stage-owner table (S + 1 <= 16), one 16-byte row
-
-// Two rows per codeword (X2): the L = 8 min-sum kernel at n = 1024 decodes 2
-// codewords per wave instead of 4, so bs = 8192 gives 4096 waves (4 per SIMD instead of 2).  Each
-// codeword owns two 16-lane DPP rows holding the same 2L candidates; the rows split the lane
-// subtree's stage buffers (row r keeps the elements j = r mod 2 of stages 1..R-1, so every f/g of
-// those stages is row-local and half as long), the 15-rotation rank (row 0 offsets 1..8, row 1
-// offsets 9..15 on a source pre-rotated by 8; one v_permlane16_swap adds the halves) and the moves
-// at a fork (each row pushes its own half of the live buffers).  The leaf value, the metric
-// penalty, the partial sums and the origin are the same in both rows.  The upper stages are
-// wave-parallel loops over (codeword, path, element) and simply run over 2 codewords.
-#ifndef PL_SCL_X2
-#define PL_SCL_X2 0
-#endif
-#ifndef PL_SCL_X2_WPE
-#define PL_SCL_X2_WPE 4  // amdgpu_waves_per_eu of the X2 kernel (4: <= 128 VGPRs, all 4096 waves of bs = 8192 resident)
-#endif
-template <int L, int V, int FM, bool FAST>
-__host__ __device__ constexpr int xrep() { return (PL_SCL_X2 && L == 8 && V == 4 && FM == 0 && !FAST) ? 2 : 1; }
 
 __host__ __device__ constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x >> 1); }
 __host__ __device__ inline int align16(int x) { return (x + 15) & ~15; }
@@ -415,101 +399,7 @@ __device__ __forceinline__ int rank16_split(double cv) {
 }
 #undef PL_RANK_ROT_A
 #undef PL_RANK_ROT_B
-// Rank from the high words alone, checked.  Metrics are non-negative doubles, so when the 16
-// candidates of a row have 16 different high words (sign, exponent, top 20 mantissa bits) the high
-// words order them exactly like the full values, and the count of smaller high words is the rank:
-// per rotation one DPP subtract (its borrow = the rotated high word is smaller) and one carry add,
-// 2 VALU instead of 3-5 plus SALU tie masks.  Equal high words (the dead paths' equal metrics of
-// the first information bits, metrics within ~2^-20 of each other) give two lanes the same count;
-// the ranks of a row then do not cover 0..15, which the OR of 1 << rank over the row shows
-// (4 DPP ORs), and the wave takes the full 64-bit stable rank instead -- the same ranks either way.
-// Same-process A/B at (512,1024), L = 8, bs = 8192: 0.848 -> 0.803 ms on N(1, 2.5^2) LLRs
-// (profiles/r05s_scl_rankhi_ab.txt), 0.850 -> 0.837 ms on the bench's AWGN LLRs at 2 dB
-// (r05u_scl_rankhi_ab_awgn.txt), bit-identical.  There the check fails more often (the CPU oracle:
-// 3.5 % of a codeword's information leaves have equal high words among the candidates, 1.8 % exactly
-// equal metrics -- LLRs of exactly 0 -- so ~13 % of the 4-codeword waves), and the branch itself
-// costs: with a trivial fallback body 0.807 ms, without the branch 0.767 ms (diagnostics
-// PL_SCL_DIAG_RANK_FB, r05w_scl_fb2_ab.txt).  The fp32 rounding of the metric as the key (ties
-// 8x rarer) measured 0.844 ms; issuing the push before the check 0.872 ms (r05v, r05w).
-#ifndef PL_SCL_RANK_HI
-#define PL_SCL_RANK_HI 1
 #endif
-#define PL_RANK_ROT_H(r)                                                                     \
-    "v_sub_co_u32_dpp %1, vcc, %3, %3 row_ror:" #r " row_mask:0xf bank_mask:0xf\n\t" \
-    "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n\t"
-__device__ __forceinline__ int rank16_hi(double cv, bool& ok) {
-    const int hi = (int)(__double_as_longlong(cv) >> 32);
-    int rk, tmp, cover;
-    asm volatile(
-        "s_nop 1\n\t"  // the DPP source was just written by a VALU
-        "v_mov_b32 %0, 0\n\t"
-        PL_RANK_ROT_H(1) PL_RANK_ROT_H(2) PL_RANK_ROT_H(3) PL_RANK_ROT_H(4) PL_RANK_ROT_H(5)
-        PL_RANK_ROT_H(6) PL_RANK_ROT_H(7) PL_RANK_ROT_H(8) PL_RANK_ROT_H(9) PL_RANK_ROT_H(10)
-        PL_RANK_ROT_H(11) PL_RANK_ROT_H(12) PL_RANK_ROT_H(13) PL_RANK_ROT_H(14) PL_RANK_ROT_H(15)
-        "v_lshlrev_b32 %2, %0, 1\n\t"
-        "s_nop 1\n\t"
-        "v_or_b32_dpp %2, %2, %2 row_ror:1 row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_or_b32_dpp %2, %2, %2 row_ror:2 row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_or_b32_dpp %2, %2, %2 row_ror:4 row_mask:0xf bank_mask:0xf\n\t"
-        "s_nop 1\n\t"
-        "v_or_b32_dpp %2, %2, %2 row_ror:8 row_mask:0xf bank_mask:0xf\n\t"
-        : "=&v"(rk), "=&v"(tmp), "=&v"(cover)
-        : "v"(hi)
-        : "vcc");
-    ok = cover == 0xffff;
-    return rk;
-}
-#undef PL_RANK_ROT_H
-#endif
-
-// ---- X2 helpers (two rows per codeword) ---------------------------------------------------
-// v_permlane16_swap(v, v) exchanges rows 2c+1 and 2c: the first result holds the even row's value
-// in both rows, the second the odd row's.  e0 / e1 = this double in the even / odd row.
-__device__ __forceinline__ void xch_rows(double v, double& e0, double& e1) {
-    const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-    const unsigned lo = (unsigned)(b & 0xffffffffull), hi = (unsigned)(b >> 32);
-    const auto rl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
-    const auto rh = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
-    e0 = __longlong_as_double((long long)(((unsigned long long)rh[0] << 32) | rl[0]));
-    e1 = __longlong_as_double((long long)(((unsigned long long)rh[1] << 32) | rl[1]));
-}
-__device__ __forceinline__ int sum_rows(int v) {
-    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
-    return (int)(r[0] + r[1]);
-}
-// Rank of this lane's candidate among the 16 of its row pair (both rows hold the same 16), the
-// stable (metric, index) order of rank16_subb.  Even rows compare against row offsets 1..8 of the
-// candidates themselves, odd rows against offsets 1..8 of a copy pre-rotated by 8 (offsets 9..16;
-// 16 is the lane itself, tie mask 0, so it counts nothing): 8 borrow-chain rotations per lane
-// instead of 15, and one v_permlane16_swap adds the two rows' counts.  The tie mask of a rotation
-// holds both rows' bits (even: lanes >= d, odd: lanes >= d + 8) in each 32-bit half of VCC.
-#define PL_RANK_ROT_X2(r, m)                                                                \
-    "s_mov_b32 vcc_lo, " #m "\n\t"                                                          \
-    "s_mov_b32 vcc_hi, " #m "\n\t"                                                          \
-    "v_subb_co_u32_dpp %1, vcc, %4, %2, vcc row_ror:" #r " row_mask:0xf bank_mask:0xf\n\t" \
-    "v_subb_co_u32_dpp %1, vcc, %5, %3, vcc row_ror:" #r " row_mask:0xf bank_mask:0xf\n\t" \
-    "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n\t"
-__device__ __forceinline__ int rank16_x2(double cv) {
-    const long long b = __double_as_longlong(cv);
-    const int lo = (int)(b & 0xffffffffLL), hi = (int)(b >> 32);
-    // the comparison source: the candidates themselves in even rows, rotated by 8 in odd rows
-    const int slo = __builtin_amdgcn_update_dpp(lo, lo, 0x128, 0xA, 0xF, false);
-    const int shi = __builtin_amdgcn_update_dpp(hi, hi, 0x128, 0xA, 0xF, false);
-    int rk, tmp;
-    asm volatile(
-        "s_nop 1\n\t"  // the DPP sources were just written by a VALU
-        "v_mov_b32 %0, 0\n\t"
-        PL_RANK_ROT_X2(1, 0xfe00fffe) PL_RANK_ROT_X2(2, 0xfc00fffc) PL_RANK_ROT_X2(3, 0xf800fff8)
-        PL_RANK_ROT_X2(4, 0xf000fff0) PL_RANK_ROT_X2(5, 0xe000ffe0) PL_RANK_ROT_X2(6, 0xc000ffc0)
-        PL_RANK_ROT_X2(7, 0x8000ff80) PL_RANK_ROT_X2(8, 0x0000ff00)
-        : "=&v"(rk), "=&v"(tmp)
-        : "v"(lo), "v"(hi), "v"(slo), "v"(shi)
-        : "vcc");
-    return sum_rows(rk);
-}
-#undef PL_RANK_ROT_X2
 
 template <int GW, int r>
 __device__ __forceinline__ void rank_rot(double cv, int gl, int lane, int& rk) {
@@ -796,67 +686,6 @@ __device__ __forceinline__ void vnode64(const St& t, const Cw& w, const float* c
         w.A[p * t.per + (1 << ls) - (1 << R) + j] = r;
     }
 }
-// vnode64 for NS = 0 (the channel level a g: the passes of the codeword's right half that start
-// from the channel) with one side at a time: the x side of every path (its results kept, one double
-// per path), then the y side and the node's f/g.  The X2 kernel's register budget (128 VGPRs):
-// both sides at once hold 32 channel values and 16 doubles per path step, which spilled.  The same
-// f/g operands and operations per element as vnode64, so the same values.
-template <int Q, int QE, int FM>  // levels Q down to QE of one side
-__device__ __forceinline__ void vside_levels(double* v, const uint32_t* bp, const int* wb, int j, int side,
-                                             uint32_t gmask, double lmax) {
-    if constexpr (Q >= QE && Q >= 0) {
-        constexpr int h = 1 << Q;
-        if ((gmask >> Q) & 1u) {
-            const uint32_t* wq = bp + wb[Q] + side;
-#pragma unroll
-            for (int m = 0; m < h; ++m) v[m] = g_op(v[m], v[m + h], (wq[2 * m] >> j) & 1u);
-        } else {
-#pragma unroll
-            for (int m = 0; m < h; ++m) v[m] = f_op<FM>(v[m], v[m + h], lmax);
-        }
-        vside_levels<Q - 1, QE, FM>(v, bp, wb, j, side, gmask, lmax);
-    }
-}
-template <int L, int V, int FM>
-__device__ __forceinline__ void vnode64_ns0(const St& t, const Cw& w, const float* ch, int co, const int* wb, int j,
-                                            uint32_t gmask, bool is_g, int pos, int ls, VCache<FM>* vc, int it,
-                                            bool w7) {
-    constexpr int H = 1 << (V - 1), NC = 2 * H, hs = 64, h = 32;
-    double xr[L];
-#pragma unroll
-    for (int side = 0; side < 2; ++side) {
-        float c[NC];
-#pragma unroll
-        for (int m = 0; m < NC; ++m) c[m] = -1.0f * ch[co + side * h + m * hs];
-#pragma unroll 1
-        for (int p = 0; p < L; ++p) {
-            const uint32_t* bp = w.beta + p * t.W;
-            double v[H];
-            const uint32_t* wq = bp + wb[V - 1] + side;
-#pragma unroll
-            for (int m = 0; m < H; ++m) v[m] = g_op((double)c[m], (double)c[m + H], (wq[2 * m] >> j) & 1u);
-            vside_levels<V - 2, 1, FM>(v, bp, wb, j, side, gmask, t.lmax);  // levels V-2 .. 1 (level 0 below)
-#if PL_SCL_C7
-            if (w7) {
-                double* e = reinterpret_cast<double*>(&vc->v7[it * L + p]) + 2 * side;
-                e[0] = v[0];
-                e[1] = v[1];
-            }
-#endif
-            if ((gmask & 1u) != 0u) v[0] = g_op(v[0], v[1], ((bp + wb[0] + side)[0] >> j) & 1u);
-            else v[0] = f_op<FM>(v[0], v[1], t.lmax);
-            if (side == 0) {
-                xr[p] = v[0];
-            } else {
-                const double x = xr[p], y = v[0];
-                if (vc != nullptr) vc->v[it * L + p] = make_double2(x, y);  // the left pass (is_g false)
-                const double r = is_g ? g_op(x, y, getbit(bp, pos + j)) : f_op<FM>(x, y, t.lmax);
-                w.A[p * t.per + (1 << ls) - (1 << R) + j] = r;
-            }
-        }
-    }
-}
-
 // The right pass from the cache: per path, the owner's (x, y) and one g.  Every owner byte, cache
 // entry and partial-sum word of the pass is loaded before the first g, so the private-memory loads
 // (L2 latency) overlap instead of being paid once per path (r04n phase timing: 12.7k cycles per pass
@@ -1013,10 +842,6 @@ __device__ void vvisit64(const St& t, int pos, bool is_g, int lane, const int* w
         const int c = idx >> ls, j = idx & (h - 1);
         const Cw w = t.cw(c);
         const int co = (int)(t.b0 + c < t.bs ? c : t.bs - 1 - t.b0) * t.n + j;
-        if constexpr (NS == 0 && CPW * 2 * L < 64) {  // X2: one side at a time (register budget)
-            vnode64_ns0<L, V, FM>(t, w, ch0, co, wb, j, gmask, is_g, pos, ls, vc, it, w7);
-            continue;
-        }
         float cx[NC], cy[NC];
 #pragma unroll
         for (int m = 0; m < NC; ++m) {
@@ -1321,8 +1146,6 @@ __device__ __forceinline__ void node_fg_st(const St& t, int pos, bool is_g, int 
 template <int L, int V, int FM, int CPW>
 __device__ void node_fg(const St& t, int s, int pos, bool is_g, int lane, VCache<FM>* vc) {
     constexpr int LL = ilog2(L);
-    if constexpr (CPW * 2 * L < 64)  // X2: per-call lane addresses (not hoisted out of the decoder loop, where
-        asm volatile("" : "+v"(lane));  // they would hold VGPRs across the lane subtrees)
     const int ls = s - 1, h = 1 << ls;
     // the per-lane cache holds kVcEntries (item, path) entries.  Release builds run pick_v's V,
     // whose virtual nodes have h <= 32 (S = 10: V = 4; S = 9: V = 3; below: h = 16), i.e. at most
@@ -1711,6 +1534,122 @@ __device__ __forceinline__ void push_live(double* st, int i, int dst, double lma
     }
 }
 
+// Selection by speculative push (PL_SCL_SPEC; 2L = 16: the L = 8 min-sum push above, and
+// select_2l's permute for the exact-f and fast-SCL kernels).  The push waits for the rank; the
+// round-5 rank from the metrics' high words also waited for its permutation check -- a chain of
+// five DPP ORs, a compare and a wave-uniform branch between the rank and the first ds_permute,
+// ~0.04 ms of the bench kernel on its own (r05w_scl_fb2_ab.txt).  Here the rank is taken on a
+// 32-bit key that is UNIQUE in the row, so it is always a permutation and every candidate is pushed
+// at once; the order is checked afterwards, on the pushed metrics, while the other pushes are
+// still in flight (same-process A/B on the bench's AWGN input, profiles/r06a/r06b_scl_spec_ab*.txt:
+// 0.836 -> 0.797 ms min-sum, 2.070 -> 2.049 ms my_sn exact f + fast-SCL):
+//   * key = 6 exponent bits (from 2^-44) and the top 22 mantissa bits of the metric, then the group
+//     lane in the low 4 bits.  In [2^-44, 2^20) the key is non-decreasing in the metric, so keys
+//     order the candidates like (metric, index) unless two metrics differ below the key's
+//     resolution (2^-22 relative; mostly metrics a few ulps apart: ~0.7 % of a codeword's
+//     information leaves at 2 dB, CPU count on the oracle); equal metrics -- the common tie, LLRs
+//     of exactly 0 and the dead paths' equal metrics -- have equal key bits and keep the index order;
+//   * after the push slot s holds the candidate of key rank s; the order is the stable (metric,
+//     index) order iff every slot's metric is >= its left neighbour's (64-bit compare, one DPP
+//     row shift per word): equal keys are in index order, so equal metrics are too;
+//   * if any row of the wave fails, the pushed candidates are ranked again by the full 64-bit
+//     stable rank (rank16_subb, the slot as the index -- equal metrics are in candidate order in
+//     the slots) and pushed once more; then the shadow slots copy their path slot as before.
+// Same selection, same values as the other forms (every SCL parity test runs this kernel).
+#ifndef PL_SCL_SPEC
+#define PL_SCL_SPEC 1
+#endif
+__device__ __forceinline__ uint32_t rank_key16(double cv, int gl) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(cv);
+    // bits 57..26 of the metric's bits minus 979 << 52: in range (2^-44 <= metric < 2^20) the 6
+    // exponent bits above 979 and 26 mantissa bits; out of range the key wraps (not monotone: the
+    // order check below catches it).  The low 4 bits are the group lane: every key is unique.
+    const uint32_t he = (uint32_t)(b >> 32) - (979u << 20);
+    const uint32_t k = __builtin_amdgcn_alignbit(he, (uint32_t)(b & 0xffffffffull), 26);
+    uint32_t r;
+    asm("v_and_or_b32 %0, %1, -16, %2" : "=v"(r) : "v"(k), "v"(gl));
+    return r;
+}
+#define PL_RANK_ROT_K(r)                                                                     \
+    "v_sub_co_u32_dpp %1, vcc, %2, %2 row_ror:" #r " row_mask:0xf bank_mask:0xf\n\t" \
+    "v_addc_co_u32_e32 %0, vcc, 0, %0, vcc\n\t"
+// rank of a unique key in its 16-lane row: per rotation one DPP subtract (borrow = the rotated key
+// is smaller) and one carry add
+__device__ __forceinline__ int rank16_key(uint32_t key) {
+    int rk, tmp;
+    asm volatile(
+        "s_nop 1\n\t"  // the DPP source was just written by a VALU
+        "v_sub_co_u32_dpp %1, vcc, %2, %2 row_ror:1 row_mask:0xf bank_mask:0xf\n\t"
+        "v_cndmask_b32_e64 %0, 0, 1, vcc\n\t"
+        PL_RANK_ROT_K(2) PL_RANK_ROT_K(3) PL_RANK_ROT_K(4) PL_RANK_ROT_K(5)
+        PL_RANK_ROT_K(6) PL_RANK_ROT_K(7) PL_RANK_ROT_K(8) PL_RANK_ROT_K(9) PL_RANK_ROT_K(10)
+        PL_RANK_ROT_K(11) PL_RANK_ROT_K(12) PL_RANK_ROT_K(13) PL_RANK_ROT_K(14) PL_RANK_ROT_K(15)
+        : "=&v"(rk), "=&v"(tmp)
+        : "v"(key)
+        : "vcc");
+    return rk;
+}
+#undef PL_RANK_ROT_K
+__device__ __forceinline__ double push_raw_d(double v, int dst) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_ds_permute(dst, (int)(b & 0xffffffffLL));
+    const int hi = __builtin_amdgcn_ds_permute(dst, (int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <int L>
+__device__ __forceinline__ int reshadow_i(int r) {
+    return __builtin_amdgcn_update_dpp(r, r, 0x120 + L, 0xF, 0xC, false);  // row_ror:8, lanes 8..15 of each row
+}
+template <int L>
+__device__ __forceinline__ double reshadow_d(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = reshadow_i<L>((int)(b & 0xffffffffLL)), hi = reshadow_i<L>((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// slot s's metric >= slot s-1's (64-bit unsigned: metrics are non-negative doubles); slot 0 of
+// each row compares with 0
+__device__ __forceinline__ bool row_order_ok(double p) {
+    const unsigned long long b = (unsigned long long)__double_as_longlong(p);
+    const uint32_t plo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffull), 0x111, 0xF, 0xF, true);
+    const uint32_t phi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0x111, 0xF, 0xF, true);
+    return (((unsigned long long)phi << 32) | plo) <= b;
+}
+// some row of the wave is out of order (rare: taken out of line)
+#if PL_DEV && defined(PL_SCL_DIAG_SPEC_FB)  // 1 = always re-rank the pushed candidates (same results), 2 = never (timing)
+#define PL_SPEC_REDO(p) \
+    (PL_SCL_DIAG_SPEC_FB == 1 || (PL_SCL_DIAG_SPEC_FB == 0 && __builtin_amdgcn_ballot_w64(!row_order_ok(p)) != 0))
+#else
+#define PL_SPEC_REDO(p) __builtin_expect(__builtin_amdgcn_ballot_w64(!row_order_ok(p)) != 0, 0)
+#endif
+// the moved live buffers (those push_live moves), without the shadow copy
+template <int s>
+__device__ __forceinline__ void push_live_raw(double* st, int i, int dst) {
+    if constexpr (s >= 1) {
+        if (((i >> (s - 1)) & 1) == 0 && !(PL_SCL_PUSH_REFM && s + 1 < R && ((i >> s) & 1) == 0)) {
+#pragma unroll
+            for (int j = 0; j < (1 << s); ++j) st[IDX(s) + j] = push_raw_d(st[IDX(s) + j], dst);
+        }
+        push_live_raw<s - 1>(st, i, dst);
+    }
+}
+// the shadow copies of the moved live buffers, then the recomputed ones (push_live's order)
+template <int L, int FM, int s>
+__device__ __forceinline__ void reshadow_live(double* st, int i, double lmax) {
+    if constexpr (s >= 1) {
+        if (((i >> (s - 1)) & 1) == 0) {
+            if (PL_SCL_PUSH_REFM && s + 1 < R && ((i >> s) & 1) == 0) {
+                constexpr int h = 1 << s, sp = s + 1 < R ? s + 1 : s;
+#pragma unroll
+                for (int j = 0; j < h; ++j) st[IDX(s) + j] = f_op<FM>(st[IDX(sp) + j], st[IDX(sp) + j + h], lmax);
+            } else {
+#pragma unroll
+                for (int j = 0; j < (1 << s); ++j) st[IDX(s) + j] = reshadow_d<L>(st[IDX(s) + j]);
+            }
+        }
+        reshadow_live<L, FM, s - 1>(st, i, lmax);
+    }
+}
+
 // Selection of the L best of the 2L candidates of a codeword group: group lane c holds candidate
 // c (c < L = (state c, u=0), c >= L = (state c-L, u=1)) with metric cv.  Its rank in the stable
 // (metric, index) order comes from 2L-1 in-group broadcasts; one ds_permute then sends every
@@ -1732,22 +1671,6 @@ __device__ __forceinline__ int rank_2l(double cv, int gl, int lane) {
             const double v = readlane_d(cv, c);
             rk += (v < cv || (v == cv && c < lane)) ? 1 : 0;
         }
-#if PL_SCL_RANK_SUBB && PL_SCL_RANK_HI
-    } else if constexpr (GW == 16) {
-        bool ok;
-        rk = rank16_hi(cv, ok);
-#if PL_DEV && defined(PL_SCL_DIAG_RANK_FB)  // timing diagnostic: 0 never / 1 always take the full rank
-        if (PL_SCL_DIAG_RANK_FB < 2) ok = PL_SCL_DIAG_RANK_FB == 0;
-#endif
-        if (__builtin_amdgcn_ballot_w64(!ok) != 0) {  // equal high words in some row: the full rank
-#if PL_DEV && defined(PL_SCL_DIAG_RANK_FB) && PL_SCL_DIAG_RANK_FB == 2  // the branch with a trivial body
-            rk = gl;
-#else
-            if constexpr (FM == 0 && PL_SCL_RANK_SPLIT) rk = rank16_split(cv);
-            else rk = rank16_subb(cv);
-#endif
-        }
-#endif
     } else if constexpr (GW == 16 && FM == 0 && PL_SCL_RANK_SUBB && PL_SCL_RANK_SPLIT) {
         rk = rank16_split(cv);  // min-sum kernels only: its 14 mask SGPRs spill the exact-f ones
     } else {
@@ -1759,13 +1682,33 @@ template <int L, int FM>
 __device__ __forceinline__ void select_2l(double cv, int gl, int gbase, int lane, double& npm, int& par,
                                           uint32_t& bit) {
     const bool hi = (gl & L) != 0;
-    const int rk = rank_2l<L, FM>(cv, gl, lane);
-    const int dst = gbase + rk;
     const int code = (gl & (L - 1)) | (hi ? 256 : 0);
-    const long long cb = __double_as_longlong(cv);
-    int rcode = __builtin_amdgcn_ds_permute(dst << 2, code);
-    int rlo = __builtin_amdgcn_ds_permute(dst << 2, (int)(cb & 0xffffffffLL));
-    int rhi = __builtin_amdgcn_ds_permute(dst << 2, (int)(cb >> 32));
+    int rcode, rlo, rhi;
+#if PL_SCL_DIAG_NO_RANK
+    if constexpr (false) {
+#else
+    if constexpr (PL_SCL_SPEC && 2 * L == 16) {
+#endif
+        // the speculative form of the push selection (rank16_key, row_order_ok): candidates go to
+        // the slot of their key rank at once, and a misordered row re-ranks the pushed candidates
+        const int dst = (gbase + rank16_key(rank_key16(cv, gl))) << 2;
+        double p = push_raw_d(cv, dst);
+        rcode = __builtin_amdgcn_ds_permute(dst, code);
+        if (PL_SPEC_REDO(p)) {
+            const int dst2 = (gbase + rank16_subb(p)) << 2;
+            p = push_raw_d(p, dst2);
+            rcode = __builtin_amdgcn_ds_permute(dst2, rcode);
+        }
+        const long long pb = __double_as_longlong(p);
+        rlo = (int)(pb & 0xffffffffLL);
+        rhi = (int)(pb >> 32);
+    } else {
+        const int dst = gbase + rank_2l<L, FM>(cv, gl, lane);
+        const long long cb = __double_as_longlong(cv);
+        rcode = __builtin_amdgcn_ds_permute(dst << 2, code);
+        rlo = __builtin_amdgcn_ds_permute(dst << 2, (int)(cb & 0xffffffffLL));
+        rhi = __builtin_amdgcn_ds_permute(dst << 2, (int)(cb >> 32));
+    }
     const int me = gbase + (gl & (L - 1));
     rcode = bperm_i(rcode, me);
     rlo = bperm_i(rlo, me);
@@ -1832,6 +1775,12 @@ __device__ __forceinline__ double node_sum_lane(const double* v, int kind, bool 
     }
 }
 
+// f(0), f(1), ..., f(sizeof...(I) - 1) with constant arguments
+template <typename F, int... I>
+__device__ __forceinline__ void unroll_leaves(F& f, std::integer_sequence<int, I...>) {
+    (f(I), ...);
+}
+
 // Decode the stage-R node at absolute position i0 for every path of every codeword of the wave
 // (group lanes < L own paths; group lanes >= L shadow lane gl - L).  pm, org: the lane's metric
 // and origin (path index inside the group).  FAST: fast-SCL pruning of the rate-0 / repetition
@@ -1848,12 +1797,12 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
     const double* inA = w.A + org * t.per;  // stage R sits at offset 0 of a path's region
     int resume = 0;                          // FAST: first leaf after a pruned node
     bool pair = false;                       // !FAST: leaf i-1 started a frozen sibling pair
-#if PL_SCL_UNROLL
-#pragma unroll
-#endif
-    for (int i = 0; i < T; ++i) {
-        if (FAST && i < resume) continue;
-        if (!FAST && PL_SCL_FROZEN_PAIR && (i & 1) && pair) continue;  // done with leaf i-1
+    // one leaf of the subtree (i: its index); !FAST kernels unroll all T leaves with constant
+    // indices (unroll_leaves) -- the loop form below was unrolled only by 8 once the body grew,
+    // which left every leaf-index shift, combine and g stage a run-time choice
+    auto leaf = [&](const int i) __attribute__((always_inline)) {
+        if (FAST && i < resume) return;
+        if (!FAST && PL_SCL_FROZEN_PAIR && (i & 1) && pair) return;  // done with leaf i-1
         if (i > 0) {  // nodes that ended at leaf i-1 (stages 1..ctz(i)): [uL ^ uR, uR] (:147-153)
             const int tz = __builtin_ctz(i);
             for (int s = 1; s <= tz; ++s) {
@@ -1912,7 +1861,7 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
                     inA = w.A + org * t.per;
                     pull_live<R - 1>(st, last, gbase + par);
                 }
-                continue;
+                return;
             }
         }
         // Frozen sibling pair (leaves i, i+1 both frozen, i even): u_i = 0 is known, so the
@@ -1942,12 +1891,39 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
                 pm = pm + pen;
             }
             PROF_MARK(9);
-            continue;
+            return;
         }
 #if PL_SCL_PROF
         asm volatile("" ::"v"(pen));
         PROF_MARK(9);
 #endif
+        if constexpr (PL_SCL_SPEC && PL_SCL_PUSH == 1 && L == 8 && FM == 0 && !PL_SCL_DIAG_NO_PULL) {
+            const double cv = pm + pen;
+            const int dst = (gbase + rank16_key(rank_key16(cv, gl))) << 2;
+            double p = push_raw_d(cv, dst);
+            int pps = __builtin_amdgcn_ds_permute(dst, (int)(ps | ((hi ? 1u : 0u) << i)));
+            int pog = __builtin_amdgcn_ds_permute(dst, org);
+            push_live_raw<R - 1>(st, i, dst);
+            if (PL_SPEC_REDO(p)) {
+                // metrics closer than the key resolves, in the wrong order: the stable 64-bit rank
+                // of the pushed candidates, and the push once more
+                const int dst2 = (gbase + rank16_subb(p)) << 2;
+                p = push_raw_d(p, dst2);
+                pps = __builtin_amdgcn_ds_permute(dst2, pps);
+                pog = __builtin_amdgcn_ds_permute(dst2, pog);
+                push_live_raw<R - 1>(st, i, dst2);
+            }
+            pm = reshadow_d<L>(p);
+            ps = (uint32_t)reshadow_i<L>(pps);
+            org = reshadow_i<L>(pog);
+            inA = w.A + org * t.per;
+            reshadow_live<L, FM, R - 1>(st, i, t.lmax);
+#if PL_SCL_PROF
+            asm volatile("" ::"v"(pm), "v"(ps), "v"(org));
+            PROF_MARK(11);
+#endif
+            return;
+        }
         if constexpr (PL_SCL_PUSH == 2 && L == 8 && FM == 0 && !PL_SCL_DIAG_NO_PULL) {
             const double cv = pm + pen;
             const int dst = (gbase + rank_2l<L, FM>(cv, gl, lane)) << 2;
@@ -1957,7 +1933,7 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
             org = bperm_i(org, src);
             inA = w.A + org * t.per;
             pull2_live<L, FM, R - 1>(st, i, src, t.lmax);
-            continue;
+            return;
         }
         if constexpr (PL_SCL_PUSH == 1 && L == 8 && FM == 0 && !PL_SCL_DIAG_NO_PULL) {  // exact f: spills (r04r)
             const double cv = pm + pen;
@@ -1975,7 +1951,7 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
             asm volatile("" ::"v"(pm), "v"(ps), "v"(org));
             PROF_MARK(11);
 #endif
-            continue;
+            return;
         }
         double npm;
         int par;
@@ -1988,6 +1964,12 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
 #if !PL_SCL_DIAG_NO_PULL  // timing diagnostic only
         pull_live<R - 1>(st, i, gbase + par);
 #endif
+    };
+    if constexpr (!FAST && PL_SCL_UNROLL) {
+        unroll_leaves(leaf, std::make_integer_sequence<int, T>{});
+    } else {
+#pragma unroll
+        for (int i = 0; i < T; ++i) leaf(i);
     }
     for (int s = 1; s <= R; ++s) {  // the nodes ending at the last leaf, up to stage R
         const int h = 1 << (s - 1), pos = T - (1 << s);
@@ -1995,133 +1977,6 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
     }
 }
 
-// The lane subtree with two rows per codeword (X2; L = 8, min-sum, no fast-SCL: the bench
-// kernel).  Row rr = (lane >> 4) & 1 of the codeword's row pair holds the elements j = 2 jl + rr
-// of the stage-3 (s3[jl], jl < 4), stage-2 (s2[jl], jl < 2) and stage-1 (s1) buffers; the f/g
-// between those stages pair elements j and j + 2^(s-1) (same parity), so they are row-local with
-// the local index jl.  The stage-1 node's two elements are exchanged between the rows (x0, x1)
-// and both rows compute the leaf value, the penalty, the rank (split between the rows) and the
-// selection; each row moves its own half of the live buffers.  Same operands, same operations and
-// same order as subtree(), so the same values.
-template <int L, int CPW>
-__device__ void subtree_x2(const St& t, int i0, uint32_t fz, double& pm, int& org, uint32_t& ps, int lane PROF_PARAM) {
-    static_assert(L == 8 && R == 4 && PL_SCL_PUSH == 1 && PL_SCL_PUSH_REFM && PL_SCL_FROZEN_PAIR,
-                  "X2: the L = 8 push-selection subtree");
-    constexpr int GW = 2 * L;
-    const int gl = lane & (GW - 1), gbase = lane & ~(GW - 1);
-    const bool hi = (gl & L) != 0;
-    const int rr = (lane >> 4) & 1;
-    const Cw w = t.cw(lane / (2 * GW));
-    const double lmax = t.lmax;
-    double s3[4], s2[2], s1 = 0.0, x0 = 0.0, x1 = 0.0;
-    ps = 0u;
-    org = gl & (L - 1);
-    const double* inA = w.A + org * t.per + rr;  // stage R at offset 0 of a path's region; this row's parity
-    bool pair = false;
-    (void)i0;
-#pragma unroll
-    for (int i = 0; i < T; ++i) {
-        if ((i & 1) && pair) continue;  // done with leaf i-1
-        if (i > 0) {  // nodes that ended at leaf i-1 (stages 1..ctz(i)): [uL ^ uR, uR]
-            const int tz = __builtin_ctz(i);
-            for (int s = 1; s <= tz; ++s) {
-                const int h = 1 << (s - 1), pos = i - (1 << s);
-                ps ^= (ps >> h) & (((1u << h) - 1u) << pos);
-            }
-            if (tz + 1 == R) inA = w.A + org * t.per + rr;  // the origin may have changed
-        }
-        // the leaf value l0 (leaf_llr): g at stage ctz(i)+1 into ctz(i), then f down
-        double l0;
-        {
-            const uint32_t psr = ps >> rr;  // bit p0 + 2 jl + rr of ps = bit p0 + 2 jl of psr
-            const int tz = i == 0 ? R : __builtin_ctz(i);
-            if (i == 0) {
-#pragma unroll
-                for (int jl = 0; jl < 4; ++jl) s3[jl] = f_ms(inA[2 * jl], inA[2 * jl + 8], lmax);
-            } else if (tz == 3) {
-#pragma unroll
-                for (int jl = 0; jl < 4; ++jl) s3[jl] = g_op(inA[2 * jl], inA[2 * jl + 8], (psr >> (2 * jl)) & 1u);
-            }
-            if (tz >= 3) {
-#pragma unroll
-                for (int jl = 0; jl < 2; ++jl) s2[jl] = f_ms(s3[jl], s3[jl + 2], lmax);
-            } else if (tz == 2) {
-                const int p0 = i - 4;
-#pragma unroll
-                for (int jl = 0; jl < 2; ++jl) s2[jl] = g_op(s3[jl], s3[jl + 2], (psr >> (p0 + 2 * jl)) & 1u);
-            }
-            if (tz >= 2) s1 = f_ms(s2[0], s2[1], lmax);
-            else if (tz == 1) s1 = g_op(s2[0], s2[1], (psr >> (i - 2)) & 1u);
-            if (tz >= 1) {
-                xch_rows(s1, x0, x1);
-                l0 = f_ms(x0, x1, lmax);
-            } else {
-                if (((fz >> (i - 1)) & 1u) == 0u) xch_rows(s1, x0, x1);  // leaf i-1 moved the state
-                l0 = g_op(x0, x1, (ps >> (i - 1)) & 1u);
-            }
-        }
-        PROF_MARK(8);
-        // frozen sibling pair: the shadow lanes take leaf i+1's value g(x0, x1, 0)
-        double lv = l0;
-        pair = (i & 1) == 0 && ((fz >> i) & 3u) == 3u;
-        if (pair && hi) lv = g_op(x0, x1, 0u);
-        const double l = fmax(fmin(lv, lmax), -lmax);
-        const bool info = ((fz >> i) & 1u) == 0u;
-        const double sl = (info && hi) ? -1.0 * l : 1.0 * l;
-        const double pen = pl::softplus_pm(-sl);
-        if (!info) {
-            if (pair) {
-                const double oth = half_xchg<L>(pen, lane);
-                pm = (pm + (hi ? oth : pen)) + (hi ? pen : oth);
-            } else {
-                pm = pm + pen;
-            }
-            PROF_MARK(9);
-            continue;
-        }
-#if PL_SCL_PROF
-        asm volatile("" ::"v"(pen));
-        PROF_MARK(9);
-#endif
-        const double cv = pm + pen;
-        const int dst = (gbase + rank16_x2(cv)) << 2;
-#if PL_SCL_PROF
-        asm volatile("" ::"v"(dst));
-        PROF_MARK(10);
-#endif
-        pm = push_d<L>(cv, dst);
-        ps = (uint32_t)push_i<L>((int)(ps | ((hi ? 1u : 0u) << i)), dst);
-        org = push_i<L>(org, dst);
-        inA = w.A + org * t.per + rr;
-        // the live buffers (left half of their node at leaf i): stage 3 moved; stage 2 / 1 the f of
-        // the moved parent when that is live too, else moved (push_live)
-        if (((i >> 2) & 1) == 0) {
-#pragma unroll
-            for (int jl = 0; jl < 4; ++jl) s3[jl] = push_d<L>(s3[jl], dst);
-        }
-        if (((i >> 1) & 1) == 0) {
-            if (((i >> 2) & 1) == 0) {
-#pragma unroll
-                for (int jl = 0; jl < 2; ++jl) s2[jl] = f_ms(s3[jl], s3[jl + 2], lmax);
-            } else {
-#pragma unroll
-                for (int jl = 0; jl < 2; ++jl) s2[jl] = push_d<L>(s2[jl], dst);
-            }
-        }
-        if ((i & 1) == 0) {
-            if (((i >> 1) & 1) == 0) s1 = f_ms(s2[0], s2[1], lmax);
-            else s1 = push_d<L>(s1, dst);
-        }
-#if PL_SCL_PROF
-        asm volatile("" ::"v"(pm), "v"(ps), "v"(org));
-        PROF_MARK(11);
-#endif
-    }
-    for (int s = 1; s <= R; ++s) {  // the nodes ending at the last leaf, up to stage R
-        const int h = 1 << (s - 1), pos = T - (1 << s);
-        ps ^= (ps >> h) & (((1u << h) - 1u) << pos);
-    }
-}
 
 // Metric term of element j of a virtual stage-s node (D = S - s stages below the channel).
 template <int D, int FM>
@@ -2303,7 +2158,7 @@ __device__ void upper_prune(const St& t, int s, int pos, int kind, double& pm, i
 template <int L, int V, int FM, bool FAST>
 __global__ __launch_bounds__(64)
 #if PL_SCL_WPE > 0
-__attribute__((amdgpu_waves_per_eu(xrep<L, V, FM, FAST>() == 2 ? PL_SCL_X2_WPE : PL_SCL_WPE)))
+__attribute__((amdgpu_waves_per_eu(PL_SCL_WPE)))
 #endif
 void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict__ out,
                                                       int out_kind, double* __restrict__ out_pm,
@@ -2311,8 +2166,7 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
                                                       const int32_t* __restrict__ info_pos, int n, int S, int k,
                                                       double lmax, int crc_deg, uint32_t crc_g,
                                                       double* __restrict__ vcache) {
-    constexpr int X = xrep<L, V, FM, FAST>();  // rows per codeword (X2: 2)
-    constexpr int GW = 2 * L, CPW = 64 / (GW * X), LL = ilog2(L);
+    constexpr int GW = 2 * L, CPW = 64 / GW, LL = ilog2(L);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = threadIdx.x;
     St t;
@@ -2329,8 +2183,7 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
     t.lmax = lmax;
     t.vcache = (FM == 1 && V >= 1 && vcache != nullptr) ? vcache + t.b0 * cache_size(n, V) : nullptr;
     const int W = t.W, LW = ilog2(W);
-    const int gl = lane & (GW - 1), my_c = lane / (GW * X);
-    const bool own = X == 1 || ((lane / GW) & (X - 1)) == 0;  // the codeword's first row writes its per-path LDS state
+    const int gl = lane & (GW - 1), my_c = lane / GW;
     const Cw mine = t.cw(my_c);
     pl::sp_load_tables(lane, 64);  // the penalty's log table (softplus.h, PL_SP_FORM 3)
     PROF_DECL;
@@ -2469,19 +2322,15 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
         } else {
             int org;
             uint32_t ps;
-            if constexpr (X == 2) {
-                subtree_x2<L, CPW>(t, i0, frozen_words[i0 >> 5] >> (i0 & 31), pm, org, ps, lane PROF_ARG);
-            } else {
-                subtree<L, FM, CPW, FAST>(t, i0, frozen_words[i0 >> 5] >> (i0 & 31), pm, org, ps, lane PROF_ARG);
-            }
+            subtree<L, FM, CPW, FAST>(t, i0, frozen_words[i0 >> 5] >> (i0 & 31), pm, org, ps, lane PROF_ARG);
             PROF_MARK(2);
             // re-point the upper-tree state of every path to its origin's, then store the
             // subtree's partial sums: partial-sum words before i0 and stage owners R..SS
-            if (gl < L && own) mine.org_s[gl] = org;
+            if (gl < L) mine.org_s[gl] = org;
             __syncthreads();
             if (!PL_SCL_DIAG_NO_REPOINT) repoint<L, V, CPW>(t, i0, lane);
             const int w_i = i0 >> 5, off = i0 & 31;
-            if (gl < L && own) {
+            if (gl < L) {
                 uint32_t* bw = mine.beta + gl * W + w_i;
                 *bw = off == 0 ? ps : ((*bw & ((1u << off) - 1u)) | (ps << off));
             }
@@ -2496,7 +2345,7 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
             for (int s = R + 1; s <= top2; ++s) combine_upper<L, CPW>(t, s, nxt - (1 << s), lane);
         PROF_MARK(4);
     }
-    if (gl < L && own) mine.pm_s[gl] = pm;
+    if (gl < L) mine.pm_s[gl] = pm;
 
     // u = x G_n per path (x = the root's partial sums): in-word spans, then word spans
     for (int idx = lane; idx < CPW * L * W; idx += 64) {
@@ -2521,7 +2370,7 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
     }
 
     // CRC check per path (my_sn dec.py:507-518)
-    if (gl < L && own) {
+    if (gl < L) {
         int f = 0;
         if (crc_deg > 0) {
             const uint32_t* U = mine.beta + gl * W;
@@ -2550,14 +2399,12 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
             rk += (v < mv || (v == mv && c < gl)) ? 1 : 0;
         }
         const double val = mv + (mine.fail_s[p] ? t.lmax * (double)k : 0.0);
-        if (own) {
-            mine.sv[rk] = val;
-            mine.sp[rk] = p;
-            if (out_pm != nullptr && t.b0 + my_c < bs) out_pm[(t.b0 + my_c) * GW + rk] = val;
-        }
+        mine.sv[rk] = val;
+        mine.sp[rk] = p;
+        if (out_pm != nullptr && t.b0 + my_c < bs) out_pm[(t.b0 + my_c) * GW + rk] = val;
     }
     __syncthreads();
-    if (gl == 0 && own) {
+    if (gl == 0) {
         double bestv = mine.sv[0];
         int best = mine.sp[0];
         for (int r = 1; r < GW; ++r)
@@ -2692,9 +2539,7 @@ int launch_scl_tree(const pl_plan* p, const float* llr, int64_t bs, void* out, i
     }
 #endif
     const Lay y = make_layout(p->n, S, L, V);
-    // codewords per wave: one 2L-lane group each, or two rows each (X2: the L = 8 min-sum kernel at V = 4)
-    const int X = (L == 8 && V == 4) ? (exact ? xrep<8, 4, 1, false>() : fast ? xrep<8, 4, 0, true>() : xrep<8, 4, 0, false>()) : 1;
-    const int cpw = 32 / L / X;
+    const int cpw = 32 / L;  // codewords per wave: one 2L-lane group each
     const int lds = cpw * y.bytes;
     if (lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);

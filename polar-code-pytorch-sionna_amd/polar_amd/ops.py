@@ -246,13 +246,17 @@ class LaunchGraph:
     once into a HIP graph and replayed as one submission.  Small batches are launch-bound: at
     (128,256) x 4096 a decode is ~7.5 us per launch issued one by one and ~6.5 us per launch
     replayed (profiles/r05i_graph_time.txt; an empty kernel: ~3 us vs ~1.7 us).  The graph
-    holds the buffers' addresses: refill the same tensors in place between replays."""
+    holds the buffers' addresses: refill the same tensors in place between replays.  The graph
+    also keeps fn -- and with it the plan, tensors and workspace its closure holds -- alive for as
+    long as it exists: a plan destroyed under a captured graph would unload the code object its
+    kernel launches come from, and freed tensors would be replayed into."""
 
     def __init__(self, fn, launches, device=None):
         if launches < 1:
             raise ValueError("launches must be >= 1")
         dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         self.launches = int(launches)
+        self.fn = fn  # keep-alive of everything the captured launches point at (see above)
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):  # one eager call first: plans load their code object lazily
@@ -265,3 +269,16 @@ class LaunchGraph:
 
     def replay(self):
         self.graph.replay()
+
+
+def shader_clock_ghz(device=None, iters=16384):
+    """The shader clock of one CU now (pl_clock_probe: one wave's dependent VALU chain timed by
+    s_memtime against the 100 MHz s_memrealtime), in GHz, measured on the current stream of
+    `device` -- so it runs right after whatever was queued before it.  Diagnostics for bench.py."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    ticks = torch.zeros(3, dtype=torch.int64, device=dev)
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().pl_clock_probe(ctypes.c_void_p(ticks.data_ptr()), int(iters),
+                                             _lib.current_stream_ptr(dev)), "pl_clock_probe")
+    t = ticks.cpu()
+    return 0.1 * float(t[0]) / max(float(t[1]), 1.0)

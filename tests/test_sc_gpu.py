@@ -299,6 +299,40 @@ def test_launch_graph_replays_bit_exact(pa):
     assert torch.equal(o8, ops.scl_decode(p8, x)), "SCL graph replay"
 
 
+def test_launch_graph_keeps_its_plan_and_buffers_alive(pa):
+    """the graph owns fn, so dropping every caller reference to the plan, the input,
+    the output and the workspace (and collecting) leaves replay() valid: the replay still writes the
+    eager decode's bits into the buffer it captured."""
+    import gc
+    import weakref
+    from polar_amd import _lib, ops
+    g = np.random.default_rng(12)
+    fp = pa.reference_frozen_pos(64, 128)
+    plan = _lib.Plan(128, pa.frozen_mask(fp, 128), 8, 0)
+    x = torch.from_numpy(g.normal(0.0, 2.0, (256, 128)).astype(np.float32)).cuda()
+    want = ops.scl_decode(plan, x)
+    out = torch.zeros((256, 64), device="cuda")
+    ws = ops.scl_workspace(plan, 256, x.device)
+    lg = ops.LaunchGraph(lambda: ops.scl_decode(plan, x, out=out, workspace=ws), 2)
+    probe = out  # the captured output buffer, read back after the replay through the closure
+    ref_plan = weakref.ref(plan)
+    del plan, x, ws, out
+    gc.collect()
+    assert ref_plan() is not None, "the graph must keep its plan alive"
+    probe.zero_()
+    lg.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(probe, want)
+
+
+def test_shader_clock_probe(pa):
+    """pl_clock_probe: s_memtime / s_memrealtime of one wave's chain gives a plausible MI355X shader
+    clock (bench.py records it around its timed region)."""
+    from polar_amd import ops
+    ghz = ops.shader_clock_ghz()
+    assert 0.5 < ghz < 3.0, ghz
+
+
 def test_sc_exact_wide_range_code_object(pa, tmp_path, monkeypatch):
     """Exact-f plans get one code object per llr_max range (exactf.h PL_EXF_RANGE): llr_max 30 and
     60 on the same code load different specialised kernels, the llr_max = 60 one compiled on demand

@@ -2,10 +2,11 @@
 
   python tools/trace_window.py KERNEL_TRACE_CSV BENCH_JSON [--kernel pl_sc_static_f32 --marker awgn_llr_kernel]
 
-bench.py launches, in order: the clock-settling steps and the --warmup steps, the --steps timed
-steps (all the decode kernel), then the Monte-Carlo iteration measurement, whose first launch is
-the producer kernel (`--marker`).  So the timed steps are the `steps` launches of the decode
-kernel immediately before the first marker launch.  Prints their average / min / max duration,
+bench.py launches, in order: the clock-settling steps and the --warmup steps, a shader-clock probe
+(`--marker`, clock_kernel), the --steps timed steps (all the decode kernel), a second probe, then
+per-launch timings and the other measurements.  So the timed steps are the decode launches between
+the first two marker launches (traces without the probe: the `steps` decode launches before the
+first launch of the Monte-Carlo producer, awgn_llr_kernel).  Prints their average / min / max duration,
 the roofline fraction that average implies (algorithmic bytes from the bench line), and the
 bench line's own HIP-event figure next to it.
 """
@@ -24,14 +25,19 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("bench_json")
     ap.add_argument("--kernel", default="pl_sc_static_f32")
-    ap.add_argument("--marker", default="awgn_llr_kernel")
+    ap.add_argument("--marker", default="clock_kernel")
     a = ap.parse_args()
     line = json.loads([ln for ln in open(a.bench_json) if ln.startswith("{")][-1])
     steps = int(line["steps"])
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
-    first_marker = next((i for i, r in enumerate(rows) if kname(r["Kernel_Name"]) == a.marker), len(rows))
-    dec = [r for r in rows[:first_marker] if kname(r["Kernel_Name"]) == a.kernel]
-    timed = dec[-steps:]
+    marks = [i for i, r in enumerate(rows) if kname(r["Kernel_Name"]) == a.marker]
+    if len(marks) >= 2:
+        dec = [r for r in rows[:marks[1]] if kname(r["Kernel_Name"]) == a.kernel]
+        timed = [r for r in rows[marks[0]:marks[1]] if kname(r["Kernel_Name"]) == a.kernel]
+    else:
+        first = next((i for i, r in enumerate(rows) if kname(r["Kernel_Name"]) == "awgn_llr_kernel"), len(rows))
+        dec = [r for r in rows[:first] if kname(r["Kernel_Name"]) == a.kernel]
+        timed = dec[-steps:]
     assert len(timed) == steps, (len(dec), steps)
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in timed]  # us
     avg = sum(dur) / len(dur)
