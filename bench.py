@@ -392,7 +392,8 @@ def valu_from_profiles(tag):
 def current_isa_sha(tag):
     """The pinned instruction-stream hash of the bench kernel (tests/golden/kernel_isa.json, which
     tests/test_kernel_resources.py holds equal to the built kernel)."""
-    pin = {"sc_k512_n1024_bs65536": "sc_k512_n1024_minsum", "scl_k512_n1024_bs8192_L8": "scl_L8_n1024_minsum"}.get(tag)
+    pin = {"sc_k512_n1024_bs65536": "sc_k512_n1024_minsum", "scl_k512_n1024_bs8192_L8": "scl_L8_n1024_minsum",
+           "scl_exact_fast_k512_n1024_bs8192_L8": "scl_L8_n1024_exact_fast"}.get(tag)
     try:
         return json.load(open(os.path.join(ROOT, "tests", "golden", "kernel_isa.json")))[pin]["sha"]
     except Exception:

@@ -179,8 +179,11 @@ def current_pins():
     with tempfile.TemporaryDirectory() as td:
         sc = isa_summary(sc_bench_asm(td), lambda n: n == "pl_sc_static_f32")
     scl = isa_summary(_scl_l8_asm(), lambda n: "scl_tree_kernelILi8ELi4ELi0ELb0E" in n)
-    assert len(sc) == 1 and len(scl) == 1, (list(sc), list(scl))
-    return {"sc_k512_n1024_minsum": list(sc.values())[0], "scl_L8_n1024_minsum": list(scl.values())[0]}
+    # my_sn SCL_Dec's default (exact f + fast-SCL; Polar5GDecoder's list decoder), the mysn_scl line
+    sclx = isa_summary(_scl_l8_asm(), lambda n: "scl_tree_kernelILi8ELi4ELi1ELb1E" in n)
+    assert len(sc) == 1 and len(scl) == 1 and len(sclx) == 1, (list(sc), list(scl), list(sclx))
+    return {"sc_k512_n1024_minsum": list(sc.values())[0], "scl_L8_n1024_minsum": list(scl.values())[0],
+            "scl_L8_n1024_exact_fast": list(sclx.values())[0]}
 
 
 def test_bench_kernel_instruction_streams_are_pinned():

@@ -13,8 +13,10 @@ import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {"sc": "pl_sc_static_f32", "scl": "scl_tree_kernel<8, 4, 0, false>"}
-KEYS = {"sc": "sc_k512_n1024_bs65536", "scl": "scl_k512_n1024_bs8192_L8"}
+KERNELS = {"sc": "pl_sc_static_f32", "scl": "scl_tree_kernel<8, 4, 0, false>", "sclx": "scl_tree_kernel<8, 4, 1, true>"}
+KEYS = {"sc": "sc_k512_n1024_bs65536", "scl": "scl_k512_n1024_bs8192_L8", "sclx": "scl_exact_fast_k512_n1024_bs8192_L8"}
+PINS = {"sc": "sc_k512_n1024_minsum", "scl": "scl_L8_n1024_minsum", "sclx": "scl_L8_n1024_exact_fast"}
+ALG = {"sc": 65536 * (4 * 1024 + 4 * 512), "scl": 8192 * (4 * 1024 + 4 * 512), "sclx": 8192 * (4 * 1024 + 4 * 512)}
 
 
 def mean_kb(path, kname):
@@ -40,7 +42,12 @@ def main(tag):
             n, m = mean_kb(os.path.join(out, f"{tag}_pmc_{dec}_{c}.csv"), kname)
             rows.append((dec, kname.replace(",", ""), c, n, m))
             kb[c] = m
-        e = tj[KEYS[dec]]
+        e = tj.setdefault(KEYS[dec], {"kernel": kname, "algorithmic_bytes_per_launch": ALG[dec],
+                                      "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes (tools/prof_pass.sh), "
+                                              "KB x1024, FETCH_SIZE doubled as for the SC kernel."})
+        # the instruction stream the counters were taken on (bench.py reports the traffic only
+        # while the built kernel still has it)
+        e["isa_sha"] = json.load(open(os.path.join(ROOT, "tests", "golden", "kernel_isa.json")))[PINS[dec]]["sha"]
         e["fetch_size_kb_per_launch"] = kb["FETCH_SIZE"]
         e["write_size_kb_per_launch"] = kb["WRITE_SIZE"]
         e["hbm_bytes_per_launch"] = int(round((2 * kb["FETCH_SIZE"] + kb["WRITE_SIZE"]) * 1024))

@@ -32,8 +32,8 @@ KERNELS = {"sc": "pl_sc_static_f32", "scl": "scl_tree_kernel<8, 4, 0, false>", "
            "sclx": "scl_tree_kernel<8, 4, 1, true>"}
 KEYS = {"sc": "sc_k512_n1024_bs65536", "scl": "scl_k512_n1024_bs8192_L8", "scx": "sc_exact_k512_n1024_bs65536",
         "sclx": "scl_exact_fast_k512_n1024_bs8192_L8"}
-# scx: the built exact-f kernel's stream (tools/isa_walk.py); sclx: stale by source hash
-PINS = {"sc": "sc_k512_n1024_minsum", "scl": "scl_L8_n1024_minsum", "scx": None, "sclx": None}
+# scx: the built exact-f kernel's stream (tools/isa_walk.py); sclx: its pinned stream (kernel_isa.json)
+PINS = {"sc": "sc_k512_n1024_minsum", "scl": "scl_L8_n1024_minsum", "scx": None, "sclx": "scl_L8_n1024_exact_fast"}
 # counter class -> calibration form(s) whose cost it carries
 CLASSES = {"SQ_INSTS_VALU_ADD_F32": "v_add_f32", "SQ_INSTS_VALU_MUL_F32": "v_mul_f32",
            "SQ_INSTS_VALU_FMA_F32": "v_fma_f32", "SQ_INSTS_VALU_TRANS_F32": "v_exp_f32",
