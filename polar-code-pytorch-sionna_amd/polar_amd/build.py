@@ -42,11 +42,13 @@ def _needs(obj, src, deps):
     return any(os.path.getmtime(d) > t for d in [src] + deps)
 
 
-def _fnv_files(paths):
+def _fnv_files(paths, extra=b""):
     h = 0xcbf29ce484222325
     for path in paths:
         for b in os.path.basename(path).encode() + b"\0" + open(path, "rb").read():
             h = ((h ^ b) * 0x100000001b3) & 0xFFFFFFFFFFFFFFFF
+    for b in extra:
+        h = ((h ^ b) * 0x100000001b3) & 0xFFFFFFFFFFFFFFFF
     return f"{h:016x}"
 
 
@@ -65,9 +67,17 @@ def source_hash():
 SCL_TREE_SOURCES = ("scl_tree_kernel.hip", "softplus.h", "plan.h")
 
 
+# the compile flags of the object files (build() below): part of what a kernel record describes
+COMPILE_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-ffp-contract=off"]
+
+
 def kernel_source_hash(files):
-    """FNV-1a 64 over the named csrc/ files and the C header, in the given order."""
-    return _fnv_files([os.path.join(CSRC, f) for f in files] + [HEADER])
+    """FNV-1a 64 over the named csrc/ files and the C header, in the given order, and the compile
+    flags and -D defines the library's units of those sources are built with (a
+    flags-only change must make the records of the kernel stale too)."""
+    defs = sorted(" ".join(d) for _, src, d in UNITS if src in files)
+    extra = (" ".join([ARCH] + COMPILE_FLAGS) + "|" + "|".join(defs)).encode()
+    return _fnv_files([os.path.join(CSRC, f) for f in files] + [HEADER], extra)
 
 
 def _write_src_hash(obj_dir):
@@ -120,8 +130,8 @@ def build(force=False, verbose=False, dev=False):
         extra = [inc] if s == "jit.cpp" else [hash_h] if s == "capi.cpp" else []
         if force or _needs(obj, src, deps + extra):
             lang = ["-x", "hip"] if s.endswith(".cpp") else []
-            cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-                   "-ffp-contract=off", f"-I{obj_dir}", f"-I{OBJ}", *dev_flags, *defs, *lang, "-c", src, "-o", obj]
+            cmd = [hipcc, f"--offload-arch={ARCH}", *COMPILE_FLAGS, f"-I{obj_dir}", f"-I{OBJ}", *dev_flags, *defs, *lang,
+                   "-c", src, "-o", obj]
             jobs.append(cmd)
 
     def run(cmd):

@@ -1888,7 +1888,7 @@ __device__ void subtree(const St& t, int i0, uint32_t fz, double& pm, int& org, 
                 const double oth = half_xchg<L>(pen, lane);
                 pm = (pm + (hi ? oth : pen)) + (hi ? pen : oth);
             } else {
-                pm = pm + pen;
+                pm = pm + pen;  // invariant: pm >= +0 (pen = softplus >= +0), which the ranks rely on
             }
             PROF_MARK(9);
             return;

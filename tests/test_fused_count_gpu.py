@@ -9,6 +9,7 @@
   * sim_ber over FusedAWGN(sim_kernel=False) + SC_Dec takes the fused-count path and its counters
     equal the two-kernel path's for the same seed (the producer-in-kernel path, pl_sc_sim_count,
     is tested in tests/test_sim_kernel_gpu.py);
+  * the same for the exact-f (my_sn SC_Dec) specialised kernels at (512,1024) and (128,256);
   * plans on the generic SC kernel report PL_ENOTSUP.
 """
 import numpy as np
@@ -25,11 +26,11 @@ def pa():
     return polar_amd
 
 
-def _plans(pa, fp, n):
+def _plans(pa, fp, n, f_mode=0):
     from polar_amd import _lib
     m = pa.frozen_mask(fp, n)
-    gen = _lib.Plan(n, m, 1, flags=_lib.PL_PLAN_GENERIC)
-    spec = _lib.Plan(n, m, 1, flags=_lib.PL_PLAN_CACHE_ONLY)
+    gen = _lib.Plan(n, m, 1, f_mode, flags=_lib.PL_PLAN_GENERIC)
+    spec = _lib.Plan(n, m, 1, f_mode, flags=_lib.PL_PLAN_CACHE_ONLY)
     assert spec.kernel()[0] == "specialized", spec.kernel()
     return gen, spec
 
@@ -50,10 +51,10 @@ def test_packed_producer_same_stream(pa):
     assert torch.equal(ub, ops.pack_bits(u))
 
 
-def _case(pa, fp, n, bs, ebno, seed):
+def _case(pa, fp, n, bs, ebno, seed, f_mode=0):
     from polar_amd import ops
     k = n - len(fp)
-    gen, spec = _plans(pa, fp, n)
+    gen, spec = _plans(pa, fp, n, f_mode)
     ub, llr = ops.awgn_qpsk_llr_bits(gen, bs, _ebno_no(ebno, k, n), seed, 0, 0)
     u, _ = ops.awgn_qpsk_llr(gen, bs, _ebno_no(ebno, k, n), seed, 0, 0)
     want = ops.count_errors(u, ops.sc_decode(spec, llr))
@@ -80,6 +81,15 @@ def test_decode_count_ragged_and_k_not_multiple_of_32(pa, k, n, bs):
     else:
         fp = pa.reference_frozen_pos(k, n).numpy()
     _case(pa, fp, n, bs, 2.0, 5)
+
+
+@pytest.mark.parametrize("k,n,bs", [(512, 1024, 8195), (128, 256, 4096)])
+def test_decode_count_exact_f(pa, k, n, bs):
+    """the exact-f specialised kernels (my_sn SC_Dec's f; n >= 128 compiles the decode +
+    count entry with the stage-(n/2) VGPR root, PL_SC_ROOT_MODE 1): sc_decode_count equals
+    count_errors of the same plan's sc_decode, ragged batch included."""
+    w = _case(pa, pa.reference_frozen_pos(k, n).numpy(), n, bs, 2.0, 17, f_mode=1)
+    assert w[1] > 0
 
 
 def test_decode_count_root_half_codes(pa):

@@ -124,6 +124,30 @@ def test_sc_bench_kernel_fits_four_waves_per_simd():
         assert m["private_segment_fixed_size"] == 0, (name, m)
 
 
+def test_sc_exact_f_bench_kernel_spill_budget():
+    """the exact-f specialised SC kernel of the BASELINE code (my_sn SC_Dec at
+    (512,1024), the mysn_sc_exact bench line) runs 3 waves per SIMD (<= 168 VGPRs) and spills at
+    most the 6 VGPRs it spilled at the end of round 5 (9 scratch instructions per wave, 32 B of
+    private memory): more spills must show up here before they show up in the timing."""
+    import polar_amd
+    from polar_amd import _lib
+    fp = polar_amd.reference_frozen_pos(512, 1024).numpy()
+    src, _ = _lib.sc_source(1024, polar_amd.frozen_mask(fp, 1024), _lib.PL_F_EXACT)
+    flags, _ = _lib._source_header(src)
+    extra = [f for f in flags if f not in ("--genco", "--no-gpu-bundle-output", "-O3", "-std=c++17",
+                                           "-ffp-contract=off") and not f.startswith("--offload-arch")]
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "sc.hip")
+        with open(path, "w") as f:
+            f.write(src)
+        asm = _compile_asm(path, extra, td)
+    meta = _kernel_meta(asm, lambda n: n == "pl_sc_static_f32")
+    (m,) = meta.values()
+    assert m["vgpr_count"] <= 168, m  # 3 waves per SIMD
+    assert m["vgpr_spill_count"] <= 6, m
+    assert m["private_segment_fixed_size"] <= 32, m
+
+
 # ---- instruction-stream pins (VERDICT r03 item 7) -------------------------------------------
 # Static instruction counts by class and a hash of the mnemonic sequence of the two bench
 # kernels, as hipcc emits them for gfx950.  A change of either kernel's code shows up here (and

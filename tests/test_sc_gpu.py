@@ -300,29 +300,35 @@ def test_launch_graph_replays_bit_exact(pa):
 
 
 def test_launch_graph_keeps_its_plan_and_buffers_alive(pa):
-    """the graph owns fn, so dropping every caller reference to the plan, the input,
-    the output and the workspace (and collecting) leaves replay() valid: the replay still writes the
-    eager decode's bits into the buffer it captured."""
+    """the graph owns fn, so once the function that captured it has returned -- its
+    plan, input and workspace referenced by nothing but the closure -- and the garbage collector
+    has run, replay() is still valid: the replay writes the eager decode's bits into the buffer it
+    captured."""
     import gc
     import weakref
     from polar_amd import _lib, ops
-    g = np.random.default_rng(12)
-    fp = pa.reference_frozen_pos(64, 128)
-    plan = _lib.Plan(128, pa.frozen_mask(fp, 128), 8, 0)
-    x = torch.from_numpy(g.normal(0.0, 2.0, (256, 128)).astype(np.float32)).cuda()
-    want = ops.scl_decode(plan, x)
-    out = torch.zeros((256, 64), device="cuda")
-    ws = ops.scl_workspace(plan, 256, x.device)
-    lg = ops.LaunchGraph(lambda: ops.scl_decode(plan, x, out=out, workspace=ws), 2)
-    probe = out  # the captured output buffer, read back after the replay through the closure
-    ref_plan = weakref.ref(plan)
-    del plan, x, ws, out
+
+    def capture():
+        g = np.random.default_rng(12)
+        fp = pa.reference_frozen_pos(64, 128)
+        plan = _lib.Plan(128, pa.frozen_mask(fp, 128), 8, 0)
+        x = torch.from_numpy(g.normal(0.0, 2.0, (256, 128)).astype(np.float32)).cuda()
+        want = ops.scl_decode(plan, x)
+        out = torch.zeros((256, 64), device="cuda")
+        ws = ops.scl_workspace(plan, 256, x.device)
+        lg = ops.LaunchGraph(lambda: ops.scl_decode(plan, x, out=out, workspace=ws), 2)
+        return lg, out, want, weakref.ref(plan)
+
+    lg, probe, want, ref_plan = capture()
     gc.collect()
     assert ref_plan() is not None, "the graph must keep its plan alive"
     probe.zero_()
     lg.replay()
     torch.cuda.synchronize()
     assert torch.equal(probe, want)
+    del lg
+    gc.collect()
+    assert ref_plan() is None, "the plan is released with the graph"
 
 
 def test_shader_clock_probe(pa):

@@ -217,3 +217,25 @@ def test_scl_dropin_module(pa):
         dec(x.to(torch.float64))  # polar_scl.py:213 asserts the input dtype
     with pytest.raises(ValueError):
         pa.SCL_Dec(d["frozen_pos"], 64, output_dtype=torch.int32)
+
+
+@pytest.mark.parametrize("f_mode,fast", [(0, False), (1, True)])
+def test_scl_metrics_are_nonnegative_doubles(pa, f_mode, fast):
+    """The invariant the 16-candidate selection rests on (scl_tree_kernel.hip rank_key16 /
+    rank16_subb compare metric BIT PATTERNS as unsigned integers): every path metric is a
+    non-negative double with a clear sign bit (no -0.0) -- pm starts at 0 or llr_max and only adds
+    softplus values >= +0.  Checked on the final sorted metrics of AWGN rows at 0 dB (many
+    equal and near-equal metrics) and of all-zero LLRs (every penalty exactly log 2)."""
+    from polar_amd import _lib, channel, ops
+    k, n = 512, 1024
+    fp = pa.reference_frozen_pos(k, n)
+    plan = _lib.Plan(n, pa.frozen_mask(fp.numpy(), n), 8, f_mode, flags=_lib.PL_PLAN_FAST_SCL if fast else 0)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    model = channel.System_AWGN_model(n, k, channel.GpuEncoder(fp, n), None, device="cuda", generator=g)
+    with torch.no_grad():
+        _, _, llr = model.llrs(2048, torch.tensor(0.0))
+    llr = torch.cat([llr.contiguous(), torch.zeros((64, n), device="cuda")])
+    _, pm = ops.scl_decode(plan, llr, return_pm=True)
+    bits = pm.view(torch.int64)
+    assert bool((bits >= 0).all()), "a metric with the sign bit set"
+    assert bool(torch.isfinite(pm).all())

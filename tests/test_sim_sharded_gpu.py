@@ -9,7 +9,8 @@ sim_ber's windowed loop.
   * configs[4] at its stated size: 8 gloo ranks x 65536 rows = 524288 codewords per iteration,
     summed counters equal one process over the same rows;
   * the RCCL backend at world size 1 (device-tensor counter all_reduce in sim_ber; bench.py's
-    barrier / timing max / BLER reduction under torch.distributed.run);
+    barrier / timing max / BLER reduction under torch.distributed.run), and at world size 2 with
+    one rank per GPU when the box has two (skipped on a one-GPU box);
   * the windowed loop equals the one-iteration loop (max_window=1) for the fused SC path and for
     an SCL decoder behind FusedAWGN (forward() + pl_count_errors);
   * the (512,1024) BLER matches the reference's measured table (x_run SC,
@@ -36,14 +37,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _sweep(rank, bs, process_group=None, max_window=None, target=TARGET):
+def _sweep(rank, bs, process_group=None, max_window=None, target=TARGET, gpu=0, ebno=EBNO, max_mc_iter=4):
     import polar_amd
     from polar_amd import channel, sim
     k, n = 512, 1024
     fp = polar_amd.reference_frozen_pos(k, n)
-    dec = polar_amd.SC_Dec(fp, n)
-    model = channel.FusedAWGN(n, k, fp, dec, device=torch.device("cuda", 0), seed=42, row0=rank * bs)
-    _, _, cnt = sim.sim_ber(model, EBNO, bs, max_mc_iter=4, target_block_errs=target, verbose=False,
+    dec = polar_amd.SC_Dec(fp, n) if gpu == 0 else polar_amd.SC_Dec(fp, n, device=torch.device("cuda", gpu))
+    model = channel.FusedAWGN(n, k, fp, dec, device=torch.device("cuda", gpu), seed=42, row0=rank * bs)
+    _, _, cnt = sim.sim_ber(model, ebno, bs, max_mc_iter=max_mc_iter, target_block_errs=target, verbose=False,
                             device="cpu", process_group=process_group, return_counts=True, max_window=max_window)
     assert model.sim_kernel, "the sweep must run the fused pl_sc_sim_count path"
     return cnt.numpy()
@@ -123,6 +124,59 @@ def test_rccl_world1_bench_line(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     assert line["n_gpus"] == 1 and line["config"]["parallelism"] == "dp1" and line["dist_backend"] == "nccl"
+    assert line["value"] > 10.0 and line["bler"] > 0.5
+
+
+def _worker_per_gpu(rank, world, port, out_dir):
+    """One rank per GPU over RCCL (xGMI): rank r on cuda:r, its shard of the keyed stream (rows
+    [r * BS, (r + 1) * BS)), one SNR point; sim_ber's [W, 4] counter all_reduce runs on the device."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "polar-code-pytorch-sionna_amd"))
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(rank)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", rank))
+    try:
+        cnt = _sweep(rank, BS, process_group=dist.group.WORLD, gpu=rank, ebno=np.array([3.0]), max_mc_iter=2)
+    finally:
+        dist.destroy_process_group()
+    np.save(os.path.join(out_dir, f"r{rank}.npy"), cnt)
+
+
+two_gpus = pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (RCCL over xGMI)")
+
+
+@two_gpus
+def test_rccl_two_gpus_sim_ber_equals_one_rank(tmp_path):
+    """RCCL at world size 2, one process per GPU (my_sn/sim.py:72-97, stop rule
+    :107-133 -- the counters the harness reduces).  Both ranks end with the same global counters,
+    equal to one process simulating both shards' rows on one GPU."""
+    import torch.multiprocessing as mp
+    world = 2
+    mp.spawn(_worker_per_gpu, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    r = [np.load(tmp_path / f"r{i}.npy") for i in range(world)]
+    np.testing.assert_array_equal(r[0], r[1])
+    one = _sweep(0, world * BS, ebno=np.array([3.0]), max_mc_iter=2)
+    np.testing.assert_array_equal(r[0], one)
+
+
+@two_gpus
+def test_rccl_two_gpus_bench_line(tmp_path):
+    """bench.py as the driver launches it at --gpus 2 (torch.distributed.run, one rank per GPU,
+    the default RCCL backend): the line reports both GPUs and the RCCL backend, and the value is
+    the whole job's throughput."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k != "PL_BENCH_BACKEND"}
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "50", "--warmup", "5", "--no-cpu-baseline", "--no-sim-iteration", "--no-configs"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["dist_backend"] == "nccl" and line["config"]["parallelism"] == "dp2"
+    assert line["config"]["global_batch"] == 2 * line["config"]["bs_per_gpu"]
     assert line["value"] > 10.0 and line["bler"] > 0.5
 
 
