@@ -143,7 +143,7 @@ __device__ __forceinline__ double pm_log(double y) {  // y >= 1, finite
 //            |r| <= ln2/2 (tail < 1.1e-16, times r^2 <= 0.12; tools/cheb_coeffs.py);
 //   log m  = 2s + s z RL(z), z = s^2 <= 0.0295, RL the degree-6 economisation of
 //            sum 2/(2i+1) z^(i-1) (tail < 3.1e-16, times s z <= 0.005);
-//   s = f / (2 + f): a reciprocal, two Newton steps and a residual correction (denominator in
+//   s = f / (2 + f): a reciprocal, PL_RCP_STEPS Newton steps and a residual correction (denominator in
 //   [1.41, 2.83]) instead of the scaled IEEE division sequence.
 // 7 fewer FMAs and a shorter division than the Taylor forms above, same accuracy class (~1 ulp).
 #ifndef PL_SP_FORM
@@ -178,6 +178,17 @@ __device__ __forceinline__ double pm_exp_e(double z) {
     }
     return ldexp(fma(r2, P, r) + 1.0, (int)k);
 }
+// Newton steps on v_rcp_f64 before the quotient's residual correction (pm_log_e, f_exact_pm_n).
+// With rc = (1 + e)/den the corrected quotient q + rc (f - den q) is (f/den)(1 - e^2): the
+// correction squares whatever error the reciprocal has left.  v_rcp_f64 is within 2^-24.4 on
+// both kernels' denominator ranges (tools/micro/rcp_check.hip, profiles/r06j_rcp_check.txt, 2.1e9
+// denominators), so after one Newton step e^2 < 2^-97 and the quotient is the two-step one on
+// every one of them (and on 2e7 host-emulated worst cases down to a 2^-20 reciprocal).  Same
+// values, two fp64 FMAs fewer per penalty and per exact f: A/B 0.759 -> 0.735 ms min-sum SCL,
+// 2.080 -> 2.021 ms my_sn SCL (profiles/r06j_scl_rcp1_ab*.txt, identical bits and metrics).
+#ifndef PL_RCP_STEPS
+#define PL_RCP_STEPS 1
+#endif
 template <bool ESTRIN>
 __device__ __forceinline__ double pm_log_e(double y) {  // y >= 1, finite
     constexpr double kLn2Hi = 0x1.62e42fefa39efp-1, kLn2Lo = 0x1.abc9e3b39803fp-56;
@@ -192,8 +203,10 @@ __device__ __forceinline__ double pm_log_e(double y) {  // y >= 1, finite
     double rc = __builtin_amdgcn_rcp(den);
     double t = fma(-den, rc, 1.0);
     rc = fma(rc, t, rc);
-    t = fma(-den, rc, 1.0);
-    rc = fma(rc, t, rc);
+    if (PL_RCP_STEPS > 1) {
+        t = fma(-den, rc, 1.0);
+        rc = fma(rc, t, rc);
+    }
     const double q = f * rc;
     const double s = fma(rc, fma(-den, q, f), q);
     const double z = s * s;
@@ -413,7 +426,7 @@ __device__ __forceinline__ double softplus_pm(double z) {
 //   f = sign(x) sign(y) (m + log(1 + E (1 - G)) - log(1 + E)) = sign(x) sign(y) (m + log1p(-t)),
 //   t = E G / (1 + E) in [0, 1/2),  log1p(-t) = 2 atanh(s),  s = -E G / (2 (1 + E) - E G),  |s| <= 1/3
 // -- one exp and one expm1 (one shared degree-9 polynomial), one quotient (denominator in [2, 4]: a
-// reciprocal with two Newton steps and a residual correction, no scaling needed) and one odd series
+// reciprocal with PL_RCP_STEPS Newton steps and a residual correction, no scaling needed) and one odd series
 // (degree 10 in s^2), ~60 VALU instead of the reference form's three exp and two general logs.  Absolute
 // error ~1e-16, against the reference's own ~1e-16 (small inputs) to ~1e-14 (|x + y| ~ 60), so
 // decisions follow the exact value at least as closely as the reference's do; parity is the
@@ -498,11 +511,13 @@ __device__ __forceinline__ void f_exact_pm_n(const double* x, const double* y, d
         rc[i] = __builtin_amdgcn_rcp(den[i]);
     }
 #pragma unroll
-    for (int i = 0; i < N; ++i) {  // s = -eg / den: two Newton steps on the reciprocal, one on the quotient
+    for (int i = 0; i < N; ++i) {  // s = -eg / den: PL_RCP_STEPS Newton steps on the reciprocal, one on the quotient
         double e = fma(-den[i], rc[i], 1.0);
         rc[i] = fma(rc[i], e, rc[i]);
-        e = fma(-den[i], rc[i], 1.0);
-        rc[i] = fma(rc[i], e, rc[i]);
+        if (PL_RCP_STEPS > 1) {
+            e = fma(-den[i], rc[i], 1.0);
+            rc[i] = fma(rc[i], e, rc[i]);
+        }
         const double q = eg[i] * rc[i];
         s[i] = -fma(rc[i], fma(-den[i], q, eg[i]), q);
         w[i] = s[i] * s[i];
