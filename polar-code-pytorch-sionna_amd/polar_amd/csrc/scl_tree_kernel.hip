@@ -96,10 +96,13 @@ namespace {
 #ifndef PL_SCL_DIAG_NO_COMBINE
 #define PL_SCL_DIAG_NO_COMBINE 0  // timing diagnostic (wrong results)
 #endif
+#ifndef PL_SCL_DIAG_VC_NOSTORE
+#define PL_SCL_DIAG_VC_NOSTORE 0  // timing diagnostic (wrong results): no virtual-node cache stores (min-sum)
+#endif
 // Diagnostic macros (timing ablations with WRONG results) exist only in development builds.
 #if !PL_DEV && (PL_SCL_DIAG_NO_UPPER || PL_SCL_DIAG_NO_UPPER_PRUNE || PL_SCL_DIAG_SKIP_V || PL_SCL_DIAG_SKIP_ST || \
                 PL_SCL_DIAG_NO_REPOINT || PL_SCL_DIAG_NO_COMBINE || PL_SCL_DIAG_NO_RANK || PL_SCL_DIAG_CHEAP_PEN || \
-                PL_SCL_DIAG_NO_PULL || PL_SCL_DIAG_FMS_ALL)
+                PL_SCL_DIAG_NO_PULL || PL_SCL_DIAG_FMS_ALL || PL_SCL_DIAG_VC_NOSTORE)
 #error "PL_SCL_DIAG_* macros give wrong results: development builds (-DPL_DEV=1) only"
 #endif
 #ifndef PL_SCL_REPOINT_VEC
@@ -672,7 +675,7 @@ __device__ __forceinline__ void vnode64(const St& t, const Cw& w, const float* c
         }
         // the stage-7 values (levels above done): cached for the right child's left pass
 #if PL_SCL_C7
-        if (w7) vc->v7[it * L + p] = make_double4(vx[0], vx[1], vy[0], vy[1]);
+        if (w7 && !PL_SCL_DIAG_VC_NOSTORE) vc->v7[it * L + p] = make_double4(vx[0], vx[1], vy[0], vy[1]);
 #endif
         if constexpr (NSS == V) {  // every level shared: nothing per path
         } else if constexpr (NS == V) {  // C7: level 0 is the last shared f (same value for every path)
@@ -681,7 +684,7 @@ __device__ __forceinline__ void vnode64(const St& t, const Cw& w, const float* c
             vlev_range<0, 0, FM>(vx, vy, bp, wb, j, gmask, t.lmax);
         }
         const double x = vx[0], y = vy[0];
-        if (vc != nullptr) vc->v[it * L + p] = make_double2(x, y);  // the left pass (is_g false)
+        if (vc != nullptr && !PL_SCL_DIAG_VC_NOSTORE) vc->v[it * L + p] = make_double2(x, y);  // the left pass (is_g false)
         const double r = is_g ? g_op(x, y, getbit(bp, pos + j)) : f_op<FM>(x, y, t.lmax);
         w.A[p * t.per + (1 << ls) - (1 << R) + j] = r;
     }
@@ -747,7 +750,7 @@ __device__ __forceinline__ void vnode64_c7(const St& t, const Cw& w, int j, int 
         for (int q = 0; q < B; ++q) {
             const double x = g_op(c[q].x, c[q].y, (wx[q] >> ((p7 + j) & 31)) & 1u);
             const double y = g_op(c[q].z, c[q].w, (wy[q] >> ((p7 + 32 + j) & 31)) & 1u);
-            vc.v[it * L + p0 + q] = make_double2(x, y);
+            if (!PL_SCL_DIAG_VC_NOSTORE) vc.v[it * L + p0 + q] = make_double2(x, y);
             w.A[(p0 + q) * t.per + (1 << ls) - (1 << R) + j] = f_ms(x, y, t.lmax);
         }
     }
@@ -757,7 +760,7 @@ __device__ __forceinline__ void vnode64_c7(const St& t, const Cw& w, int j, int 
         const uint32_t* bp = w.beta + p * t.W;
         const double4 c = vc.v7[it * L + w.sptr[p * SPS + ls + 2]];
         const double x = g_op(c.x, c.y, getbit(bp, p7 + j)), y = g_op(c.z, c.w, getbit(bp, p7 + 32 + j));
-        vc.v[it * L + p] = make_double2(x, y);
+        if (!PL_SCL_DIAG_VC_NOSTORE) vc.v[it * L + p] = make_double2(x, y);
         w.A[p * t.per + (1 << ls) - (1 << R) + j] = f_ms(x, y, t.lmax);
     }
 #endif
