@@ -165,13 +165,18 @@ def test_mysn_sc_module(pa):
 
 @pytest.mark.parametrize("kernel", ["subtree", "generic"])
 @pytest.mark.parametrize("fast", [True, False])
-def test_mysn_scl_crc_llr_max_vs_oracle(pa, kernel, fast):
+@pytest.mark.parametrize("L,lmax", [(4, 7.5), (8, 7.5), (8, 300.0)])
+def test_mysn_scl_crc_llr_max_vs_oracle(pa, kernel, fast, L, lmax):
     """llr_max != 30 (my_sn dec.py:213 self._llr_max): it clips f and the metric terms, sets the
     dead-path metric (:420-422) and the CRC penalty llr_max*k (:517).  Min-sum f: bit-exact and
-    metrics to 1e-9 against the oracle run with the same llr_max, on both SCL kernels."""
+    metrics to 1e-9 against the oracle run with the same llr_max, on both SCL kernels.  At L = 8 the
+    subtree kernel selects by the speculative push (scl_tree_kernel.hip PL_SCL_SPEC), whose key
+    covers metrics in [2^-44, 2^20): llr_max = 300 makes metrics far below 2^-44 (softplus(-300) ~
+    5e-131), outside the key's range, where only the order check and the 64-bit re-rank keep the
+    selection exact."""
     from polar_amd import _lib, ops
     from polar_amd.mysn import crc_params
-    k, n, L, lmax = 128, 256, 4, 7.5
+    k, n = 128, 256
     fp = pa.reference_frozen_pos(k, n).numpy()
     rng = np.random.default_rng(17)
     u = oracle.crc_encode(rng.integers(0, 2, (160, k - 11)).astype(np.float32), "CRC11")
