@@ -145,11 +145,23 @@ struct Prof {
         (P).t = prof_n;                                              \
     } while (0)
 #define PROF_MARK(i) PROF_MARK_P(prof, i)
+// sub-phases of the exact-f virtual pass (vvisit_ex), reported in the slots the FAST kernels leave
+// empty: 8 = cache / channel loads (waited for), 10 = the four-outcome f, 11 = the per-path levels
+__shared__ unsigned long long vex_prof[3];
+#define VEX_T0 unsigned long long vex_t = __builtin_amdgcn_s_memtime()
+#define VEX_MARK(i)                                                            \
+    do {                                                                       \
+        const unsigned long long vex_n = __builtin_amdgcn_s_memtime();         \
+        if (lane == 0) vex_prof[i] += vex_n - vex_t;                           \
+        vex_t = vex_n;                                                         \
+    } while (0)
 #define PROF_PARAM , Prof& prof
 #define PROF_ARG , prof
 #else
 #define PROF_DECL
 #define PROF_MARK(i)
+#define VEX_T0
+#define VEX_MARK(i)
 #define PROF_PARAM
 #define PROF_ARG
 #endif
@@ -872,6 +884,13 @@ __device__ void vvisit64(const St& t, int pos, bool is_g, int lane, const int* w
 #ifndef PL_SCL_FEX_COMBO
 #define PL_SCL_FEX_COMBO 1  // 1: the f level after the first per-path g from its four path-independent outcomes
 #endif
+template <int Q, typename F>
+__device__ __forceinline__ void vex_levels(F& level) {  // level(Q), level(Q - 1), ..., level(0)
+    if constexpr (Q >= 0) {
+        level(std::integral_constant<int, Q>{});
+        vex_levels<Q - 1>(level);
+    }
+}
 #ifndef PL_SCL_FEX_INL
 #define PL_SCL_FEX_INL 1  // 1: vvisit_ex inlined (register arrays via s_set_gpr_idx); 0: out of line (A/B r03i:
                           // callee register saves through scratch every pass, 4.10 vs 3.71 ms)
@@ -903,9 +922,10 @@ __device__ PL_FEX_PASS_ATTR void vvisit_ex(const float* __restrict__ llr, int64_
     int ns = 0;  // leading f levels (uniform)
     while (ns < V && ((gmask >> (V - 1 - ns)) & 1u) == 0u) ++ns;
     const float* ch0 = llr + b0 * n;
-    // Register arrays as vector values: a dynamic (uniform) index lowers to s_set_gpr_idx moves,
-    // never to scratch (a plain local array in an out-of-line function goes to the stack).
-    typedef double lv __attribute__((ext_vector_type(H)));
+    // The pass's register blocks (wx, wy) are vector values, so the dynamic (uniform) indices of
+    // the no-workspace fallback loops below stay in registers (as compare-and-select chains, slow
+    // but rare: the product path always passes the workspace); the workspace paths and the
+    // per-path levels use compile-time indices only.
     const int q1 = V - 1 - ns, h1 = 1 << (q1 > 0 ? q1 : 0), h2 = h1 >> 1;
     // First per-path level q1 (a g) followed by an f: each input of that f is one of two
     // path-independent sums (g with u = 0 or 1), so its four outcomes per element are computed
@@ -946,11 +966,12 @@ __device__ PL_FEX_PASS_ATTR void vvisit_ex(const float* __restrict__ llr, int64_
 #endif
             continue;
         }
+        VEX_T0;
         const int co = (int)(b0 + c < bs ? c : bs - 1 - b0) * n + j;
         // One register block per side holds what the path loop reads: the channel elements
         // j + m 2^s (x; y: + 2^(s-1)) as doubles when the channel level is per path (ns = 0), the
         // shared level-ns values (ns > 0), or the four-outcome table w[m + (2 b1 + b2) h2] (combo).
-        wv wx, wy;
+        double wx[NC], wy[NC];  // constant indices only: SROA keeps every entry its own register
         int hh = NC;
         const bool tab = combo && vcache != nullptr;  // the four-outcome table from the workspace
         if (tab) {
@@ -993,59 +1014,93 @@ __device__ PL_FEX_PASS_ATTR void vvisit_ex(const float* __restrict__ llr, int64_
                     wy[m] = cb[h + m * hs];
                 }
             }
-        } else if (ns > 0) {  // shared levels V-1 .. V-ns evaluated here
+        }
+#if PL_SCL_PROF
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        VEX_MARK(0);
+#endif
+        if (vcache == nullptr && (ns > 0 || combo)) {
+            // no workspace: the shared levels and the four-outcome step here, on vector copies
+            // whose dynamic (uniform) indices stay in registers (compare-and-select chains)
+            wv fx, fy;
+#pragma unroll
+            for (int m = 0; m < NC; ++m) {
+                fx[m] = wx[m];
+                fy[m] = wy[m];
+            }
+            if (ns > 0) {  // shared levels V-1 .. V-ns
 #pragma unroll 1
-            for (int q = V - 1; q >= V - ns; --q) {
-                hh = 1 << q;
+                for (int q = V - 1; q >= V - ns; --q) {
+                    hh = 1 << q;
 #pragma unroll 1
-                for (int m = 0; m < hh; ++m) {
-                    double a, b;
-                    f_ex2(wx[m], wx[m + hh], wy[m], wy[m + hh], lmax, a, b);
-                    wx[m] = a;
-                    wy[m] = b;
+                    for (int m = 0; m < hh; ++m) {
+                        double a, b;
+                        f_ex2(fx[m], fx[m + hh], fy[m], fy[m + hh], lmax, a, b);
+                        fx[m] = a;
+                        fy[m] = b;
+                    }
                 }
             }
-        }
-        if (combo && !tab) {  // in place: block m reads and writes exactly the indices m + k h2, k < 4
+            if (combo) {  // in place: block m reads and writes exactly the indices m + k h2, k < 4
 #pragma unroll 1
-            for (int m = 0; m < h2; ++m) {
-                const double xa = wx[m], xb = wx[m + h1], xc_ = wx[m + h2], xd = wx[m + h2 + h1];
-                const double ya = wy[m], yb = wy[m + h1], yc_ = wy[m + h2], yd = wy[m + h2 + h1];
-                const double gx0 = g_op(xa, xb, 0u), gx1 = g_op(xa, xb, 1u);
-                const double hx0 = g_op(xc_, xd, 0u), hx1 = g_op(xc_, xd, 1u);
-                const double gy0 = g_op(ya, yb, 0u), gy1 = g_op(ya, yb, 1u);
-                const double hy0 = g_op(yc_, yd, 0u), hy1 = g_op(yc_, yd, 1u);
-                double r0, r1, r2, r3, t0, t1, t2, t3;
-                f_ex2(gx0, hx0, gx0, hx1, lmax, r0, r1);
-                f_ex2(gx1, hx0, gx1, hx1, lmax, r2, r3);
-                f_ex2(gy0, hy0, gy0, hy1, lmax, t0, t1);
-                f_ex2(gy1, hy0, gy1, hy1, lmax, t2, t3);
-                wx[m] = r0;
-                wx[m + h2] = r1;
-                wx[m + 2 * h2] = r2;
-                wx[m + 3 * h2] = r3;
-                wy[m] = t0;
-                wy[m + h2] = t1;
-                wy[m + 2 * h2] = t2;
-                wy[m + 3 * h2] = t3;
+                for (int m = 0; m < h2; ++m) {
+                    const double xa = fx[m], xb = fx[m + h1], xc_ = fx[m + h2], xd = fx[m + h2 + h1];
+                    const double ya = fy[m], yb = fy[m + h1], yc_ = fy[m + h2], yd = fy[m + h2 + h1];
+                    const double gx0 = g_op(xa, xb, 0u), gx1 = g_op(xa, xb, 1u);
+                    const double hx0 = g_op(xc_, xd, 0u), hx1 = g_op(xc_, xd, 1u);
+                    const double gy0 = g_op(ya, yb, 0u), gy1 = g_op(ya, yb, 1u);
+                    const double hy0 = g_op(yc_, yd, 0u), hy1 = g_op(yc_, yd, 1u);
+                    double r0, r1, r2, r3, t0, t1, t2, t3;
+                    f_ex2(gx0, hx0, gx0, hx1, lmax, r0, r1);
+                    f_ex2(gx1, hx0, gx1, hx1, lmax, r2, r3);
+                    f_ex2(gy0, hy0, gy0, hy1, lmax, t0, t1);
+                    f_ex2(gy1, hy0, gy1, hy1, lmax, t2, t3);
+                    fx[m] = r0;
+                    fx[m + h2] = r1;
+                    fx[m + 2 * h2] = r2;
+                    fx[m + 3 * h2] = r3;
+                    fy[m] = t0;
+                    fy[m + h2] = t1;
+                    fy[m + 2 * h2] = t2;
+                    fy[m + 3 * h2] = t3;
+                }
+            }
+#pragma unroll
+            for (int m = 0; m < NC; ++m) {
+                wx[m] = fx[m];
+                wy[m] = fy[m];
             }
         }
+        VEX_MARK(1);
+        // Per-path levels with compile-time register indices: level q (2^q pairs) is its own
+        // unrolled block, entered when q <= q0 (uniform), f or g by gmask (uniform).  (Round 6:
+        // the loop form's dynamic indices into the register blocks lowered to compare-and-select
+        // chains over every entry per access -- ~100 VALU per f pair, and the four-outcome pick
+        // to a 16-way chain per value; A/B 2.03 -> 1.88 ms, bit-identical,
+        // profiles/r06t_unr_ab_mysn.txt.)
 #pragma unroll 1
         for (int p = 0; p < L; ++p) {
             const uint32_t* bp = beta + p * W;
-            lv vx, vy;
-            int q0;  // first per-path level
+            // an opaque per-path copy of the element index: the partial-sum addresses and shifts
+            // derived from it are recomputed per path, not hoisted out of the loop (~50 VGPRs)
+            int jo = j;
+            asm volatile("" : "+v"(jo));
+            double vx[H], vy[H];
+            int q0;
             if (combo) {
-                const int ox = bx[q1] + j, oy = by[q1] + j;
-                // static register indices per table size (h2 = 1, 2, 4: a uniform branch)
+                const int ox = bx[q1] + jo, oy = by[q1] + jo;
                 auto pick = [&](auto H2c) {
                     constexpr int H2 = decltype(H2c)::value;
 #pragma unroll
                     for (int m = 0; m < H2; ++m) {
                         const uint32_t bx1 = getbit(bp, ox + m * hs), bx2 = getbit(bp, ox + (m + H2) * hs);
                         const uint32_t by1 = getbit(bp, oy + m * hs), by2 = getbit(bp, oy + (m + H2) * hs);
-                        vx[m] = bx1 ? (bx2 ? wx[m + 3 * H2] : wx[m + 2 * H2]) : (bx2 ? wx[m + H2] : wx[m]);
-                        vy[m] = by1 ? (by2 ? wy[m + 3 * H2] : wy[m + 2 * H2]) : (by2 ? wy[m + H2] : wy[m]);
+                        double x0 = wx[m], x1 = wx[m + H2], x2 = wx[m + 2 * H2], x3 = wx[m + 3 * H2];
+                        double y0 = wy[m], y1 = wy[m + H2], y2 = wy[m + 2 * H2], y3 = wy[m + 3 * H2];
+                        asm volatile("" : "+v"(x0), "+v"(x1), "+v"(x2), "+v"(x3));
+                        asm volatile("" : "+v"(y0), "+v"(y1), "+v"(y2), "+v"(y3));
+                        vx[m] = bx1 ? (bx2 ? x3 : x2) : (bx2 ? x1 : x0);
+                        vy[m] = by1 ? (by2 ? y3 : y2) : (by2 ? y1 : y0);
                     }
                 };
                 if constexpr (H >= 8) {
@@ -1057,45 +1112,46 @@ __device__ PL_FEX_PASS_ATTR void vvisit_ex(const float* __restrict__ llr, int64_
                 if (h2 == 1) pick(std::integral_constant<int, 1>{});
                 q0 = q1 - 2;
             } else if (ns == 0) {  // the channel level is a g
-#pragma unroll 1
+#pragma unroll
                 for (int m = 0; m < H; ++m) {
-                    vx[m] = g_op(wx[m], wx[m + H], getbit(bp, bx[V - 1] + j + m * hs));
-                    vy[m] = g_op(wy[m], wy[m + H], getbit(bp, by[V - 1] + j + m * hs));
+                    vx[m] = g_op(wx[m], wx[m + H], getbit(bp, bx[V - 1] + jo + m * hs));
+                    vy[m] = g_op(wy[m], wy[m + H], getbit(bp, by[V - 1] + jo + m * hs));
                 }
                 q0 = V - 2;
             } else {
-#pragma unroll 1
-                for (int m = 0; m < hh; ++m) {
+#pragma unroll
+                for (int m = 0; m < H; ++m) {  // entries past hh are never read
                     vx[m] = wx[m];
                     vy[m] = wy[m];
                 }
                 q0 = V - 1 - ns;
             }
-#pragma unroll 1
-            for (int q = q0; q >= 0; --q) {
-                const int hq = 1 << q;
-                const int ox = bx[q] + j, oy = by[q] + j;
-                if ((gmask >> q) & 1u) {
-#pragma unroll 1
-                    for (int m = 0; m < hq; ++m) {
-                        vx[m] = g_op(vx[m], vx[m + hq], getbit(bp, ox + m * hs));
-                        vy[m] = g_op(vy[m], vy[m + hq], getbit(bp, oy + m * hs));
+            auto level = [&](auto Qc) {
+                constexpr int Q = decltype(Qc)::value, HQ = 1 << Q;
+                if (Q > q0) return;
+                const int ox = bx[Q] + jo, oy = by[Q] + jo;
+                // with the four-outcome step, a per-path f level lies at least two levels below
+                // the first per-path g (q1 <= V - 1): level V - 2 is always a g
+                if (((gmask >> Q) & 1u) || (PL_SCL_FEX_COMBO && Q > V - 3)) {
+#pragma unroll
+                    for (int m = 0; m < HQ; ++m) {
+                        vx[m] = g_op(vx[m], vx[m + HQ], getbit(bp, ox + m * hs));
+                        vy[m] = g_op(vy[m], vy[m + HQ], getbit(bp, oy + m * hs));
                     }
                 } else {
-#pragma unroll 1
-                    for (int m = 0; m < hq; ++m) {
-                        double a, b;
-                        f_ex2(vx[m], vx[m + hq], vy[m], vy[m + hq], lmax, a, b);
-                        vx[m] = a;
-                        vy[m] = b;
+#pragma unroll
+                    for (int m = 0; m < HQ; ++m) {
+                        f_ex2(vx[m], vx[m + HQ], vy[m], vy[m + HQ], lmax, vx[m], vy[m]);
                     }
                 }
-            }
+            };
+            vex_levels<V - 2>(level);
             const double x = vx[0], y = vy[0];
             if (vc != nullptr) vc->v[it * L + p] = make_double2(x, y);  // the left pass
-            const double r = is_g ? g_op(x, y, getbit(bp, pos + j)) : f_ex(x, y, lmax);
+            const double r = is_g ? g_op(x, y, getbit(bp, pos + jo)) : f_ex(x, y, lmax);
             A[p * per + (1 << ls) - (1 << R) + j] = r;
         }
+        VEX_MARK(2);
     }
 }
 
@@ -2189,7 +2245,12 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
     const int gl = lane & (GW - 1), my_c = lane / GW;
     const Cw mine = t.cw(my_c);
     pl::sp_load_tables(lane, 64);  // the penalty's log table (softplus.h, PL_SP_FORM 3)
+    pl::fex_load_table<FM == 1>(lane);  // the exact f's 2^(j/64) table (softplus.h, PL_FEX_TAB)
     PROF_DECL;
+#if PL_SCL_PROF
+    if (lane < 3) vex_prof[lane] = 0ull;
+    __syncthreads();
+#endif
 
     for (int i = lane; i < CPW * L * W; i += 64) t.cw(i >> (LL + LW)).beta[i & (L * W - 1)] = 0u;
     for (int i = lane; i < CPW * L * SPS; i += 64) {
@@ -2432,6 +2493,11 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
     }
 #if PL_SCL_PROF
     PROF_MARK(7);
+    if constexpr (FM == 1 && FAST) {  // the vvisit_ex sub-phases (inside slot 0's time)
+        prof.acc[8] = vex_prof[0];
+        prof.acc[10] = vex_prof[1];
+        prof.acc[11] = vex_prof[2];
+    }
     if (out_pm != nullptr && lane < kProfSlots) {
         unsigned long long v = prof.acc[0];
 #pragma unroll

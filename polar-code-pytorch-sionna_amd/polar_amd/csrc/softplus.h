@@ -425,9 +425,9 @@ __device__ __forceinline__ double softplus_pm(double z) {
 // m = min(a, b), M = max(a, b), E = e^-(M-m), G = 1 - e^-2m (= -expm1(-2m)):
 //   f = sign(x) sign(y) (m + log(1 + E (1 - G)) - log(1 + E)) = sign(x) sign(y) (m + log1p(-t)),
 //   t = E G / (1 + E) in [0, 1/2),  log1p(-t) = 2 atanh(s),  s = -E G / (2 (1 + E) - E G),  |s| <= 1/3
-// -- one exp and one expm1 (one shared degree-9 polynomial), one quotient (denominator in [2, 4]: a
+// -- two table-driven exponentials (fex_exp below), one quotient (denominator in [2, 4]: a
 // reciprocal with PL_RCP_STEPS Newton steps and a residual correction, no scaling needed) and one odd series
-// (degree 10 in s^2), ~60 VALU instead of the reference form's three exp and two general logs.  Absolute
+// (degree 10 in s^2), ~65 VALU instead of the reference form's three exp and two general logs.  Absolute
 // error ~1e-16, against the reference's own ~1e-16 (small inputs) to ~1e-14 (|x + y| ~ 60), so
 // decisions follow the exact value at least as closely as the reference's do; parity is the
 // statistical row-mismatch gate of tests/test_exactf_gpu.py.
@@ -454,58 +454,81 @@ __device__ __forceinline__ double vmax_abs_nc(double a, double b) {
     asm("v_max_f64 %0, |%1|, |%2|" : "=v"(d) : "v"(a), "v"(b));
     return d;
 }
+// The exact f's two exponentials come from a 64-entry table of 2^(j/64) in LDS (fex_tab, loaded by
+// fex_load_table() at kernel entry in the exact-f kernels): z = N ln2/64 + r by the 1.5 2^52 shifter
+// (N in its low word, no rint / conversion), |r| <= ln2/128, e^r - 1 by degree 5 (round 6; until
+// then Cody-Waite to |r| <= ln2/2 and degree 9: 75 -> 65 VALU per f, fewer constants, and with them
+// fewer SGPR / VGPR spills in the list kernels -- my_sn SCL default 1.79 -> 1.65 ms,
+// profiles/r06w_tab_ab_mysn.txt).  Host accuracy check of both forms against binary128:
+// tools/micro/fex_tab_check.cpp (the same largest absolute error; the table form's errors ~10 %
+// larger on average, far below the reference's own cancellation error).
+__device__ const double kFexTab[64] = {
+    0x1.0000000000000p+0, 0x1.02c9a3e778061p+0, 0x1.059b0d3158574p+0, 0x1.0874518759bc8p+0,
+    0x1.0b5586cf9890fp+0, 0x1.0e3ec32d3d1a2p+0, 0x1.11301d0125b51p+0, 0x1.1429aaea92de0p+0,
+    0x1.172b83c7d517bp+0, 0x1.1a35beb6fcb75p+0, 0x1.1d4873168b9aap+0, 0x1.2063b88628cd6p+0,
+    0x1.2387a6e756238p+0, 0x1.26b4565e27cddp+0, 0x1.29e9df51fdee1p+0, 0x1.2d285a6e4030bp+0,
+    0x1.306fe0a31b715p+0, 0x1.33c08b26416ffp+0, 0x1.371a7373aa9cbp+0, 0x1.3a7db34e59ff7p+0,
+    0x1.3dea64c123422p+0, 0x1.4160a21f72e2ap+0, 0x1.44e086061892dp+0, 0x1.486a2b5c13cd0p+0,
+    0x1.4bfdad5362a27p+0, 0x1.4f9b2769d2ca7p+0, 0x1.5342b569d4f82p+0, 0x1.56f4736b527dap+0,
+    0x1.5ab07dd485429p+0, 0x1.5e76f15ad2148p+0, 0x1.6247eb03a5585p+0, 0x1.6623882552225p+0,
+    0x1.6a09e667f3bcdp+0, 0x1.6dfb23c651a2fp+0, 0x1.71f75e8ec5f74p+0, 0x1.75feb564267c9p+0,
+    0x1.7a11473eb0187p+0, 0x1.7e2f336cf4e62p+0, 0x1.82589994cce13p+0, 0x1.868d99b4492edp+0,
+    0x1.8ace5422aa0dbp+0, 0x1.8f1ae99157736p+0, 0x1.93737b0cdc5e5p+0, 0x1.97d829fde4e50p+0,
+    0x1.9c49182a3f090p+0, 0x1.a0c667b5de565p+0, 0x1.a5503b23e255dp+0, 0x1.a9e6b5579fdbfp+0,
+    0x1.ae89f995ad3adp+0, 0x1.b33a2b84f15fbp+0, 0x1.b7f76f2fb5e47p+0, 0x1.bcc1e904bc1d2p+0,
+    0x1.c199bdd85529cp+0, 0x1.c67f12e57d14bp+0, 0x1.cb720dcef9069p+0, 0x1.d072d4a07897cp+0,
+    0x1.d5818dcfba487p+0, 0x1.da9e603db3285p+0, 0x1.dfc97337b9b5fp+0, 0x1.e502ee78b3ff6p+0,
+    0x1.ea4afa2a490dap+0, 0x1.efa1bee615a27p+0, 0x1.f50765b6e4540p+0, 0x1.fa7c1819e90d8p+0,
+};
+__shared__ double fex_tab[64];
+template <bool ON>
+__device__ __forceinline__ void fex_load_table(int tid) {  // one wave: lane i loads 2^(i/64)
+    if constexpr (ON) {
+        fex_tab[tid & 63] = kFexTab[tid & 63];
+        __syncthreads();
+    }
+}
+// e^z for z <= 0 (z >= -2000) as 2^k T (1 + q): A = 2^k T (exact), q = e^r - 1
+__device__ __forceinline__ void fex_exp(double z, double& A, double& q) {
+    constexpr double kInv = 0x1.71547652b82fep+6, kCHi = 0x1.62e42fefa39efp-7, kCLo = 0x1.abc9e3b39803fp-62;
+    const double t = __builtin_fma(z, kInv, 0x1.8p52);
+    const int n = (int)(uint32_t)(unsigned long long)__double_as_longlong(t);
+    const double nd = t - 0x1.8p52;
+    double r = __builtin_fma(-nd, kCHi, z);
+    r = __builtin_fma(-nd, kCLo, r);
+    const double r2 = r * r;
+    double h = __builtin_fma(1.0 / 120.0, r, 1.0 / 24.0);
+    h = __builtin_fma(h, r, 1.0 / 6.0);
+    h = __builtin_fma(h, r, 0.5);
+    q = __builtin_fma(r2, h, r);
+    A = __builtin_ldexp(fex_tab[n & 63], n >> 6);
+}
 template <int N>
 __device__ __forceinline__ void f_exact_pm_n(const double* x, const double* y, double lmax, double* out) {
-    constexpr double kLog2e = 1.4426950408889634;
-    constexpr double kLn2Hi = 0x1.62e42fefa39efp-1, kLn2Lo = 0x1.abc9e3b39803fp-56;
     // 2 atanh(s) = 2s + s w R(w), w = s^2 <= 1/9: R of degree 10, the Chebyshev economisation of
     // sum 2/(2i+3) w^i (tail < 2.4e-18)
     constexpr double kS[11] = {
         0.6666666666666666, 0.39999999999999514, 0.28571428571603413, 0.22222222197853667,
         0.18181819920440906, 0.15384543207664578, 0.133351941539121, 0.11734082174871642,
         0.10846687166200544, 0.07485743922141379, 0.1564211337480669};
-    double m[N], ze[N], zm[N], ke[N], km[N], re[N], rm[N], pe[N], pm[N];
-    bool neg[N];
+    double m[N], E[N], G[N];
+    uint32_t sg[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-        const double xc = vmax_nc(vmin_nc(x[i], lmax), -lmax), yc = vmax_nc(vmin_nc(y[i], lmax), -lmax);
-        neg[i] = (__double_as_longlong(xc) ^ __double_as_longlong(yc)) < 0;
-        m[i] = vmin_abs_nc(xc, yc);
-        ze[i] = m[i] - vmax_abs_nc(xc, yc);  // -(M - m) <= 0
-        zm[i] = -2.0 * m[i];
+        // |clip(v, +-lmax)| = min(|v|, lmax): m and M straight from the magnitudes
+        m[i] = vmin_nc(vmin_abs_nc(x[i], y[i]), lmax);
+        const double M = vmin_nc(vmax_abs_nc(x[i], y[i]), lmax);
+        sg[i] = ((uint32_t)((unsigned long long)__double_as_longlong(x[i]) >> 32) ^
+                 (uint32_t)((unsigned long long)__double_as_longlong(y[i]) >> 32)) & 0x80000000u;
+        double Ae, qe, Am, qm;
+        fex_exp(vmax_nc(m[i] - M, -2000.0), Ae, qe);  // e^-2000 = 0 like e^-745: n stays in int range
+        fex_exp(vmax_nc(-2.0 * m[i], -2000.0), Am, qm);
+        E[i] = __builtin_fma(Ae, qe, Ae);              // exp(-(M - m))
+        G[i] = __builtin_fma(-Am, qm, 1.0 - Am);       // -expm1(-2m); 1 - Am exact (Am in [1/2, 1] or G > 1/2)
     }
-    // exp(r) = 1 + r + r^2 P(r), expm1(r) = r + r^2 P(r), |r| <= ln2/2: P of degree 9, the Chebyshev
-    // economisation of the Taylor series of (e^r - 1 - r) / r^2 (tail < 1.1e-16, times r^2 <= 0.12);
-    // the coefficients and the economised series below: tools/cheb_coeffs.py
-    constexpr double kP[10] = {
-        0.5000000000000001, 0.1666666666666667, 0.04166666666662413, 0.008333333333326136,
-        0.001388888891721154, 0.00019841269874817515, 2.4801521299750923e-05, 2.75572554044176e-06,
-        2.7620086491464514e-07, 2.5105215165649368e-08};
-#pragma unroll
-    for (int i = 0; i < N; ++i) {  // Cody-Waite reductions of both exponents
-        ke[i] = __builtin_rint(ze[i] * kLog2e);
-        km[i] = __builtin_rint(zm[i] * kLog2e);
-        re[i] = fma(-ke[i], kLn2Hi, ze[i]);
-        rm[i] = fma(-km[i], kLn2Hi, zm[i]);
-        re[i] = fma(-ke[i], kLn2Lo, re[i]);
-        rm[i] = fma(-km[i], kLn2Lo, rm[i]);
-        pe[i] = kP[9];
-        pm[i] = kP[9];
-    }
-#pragma unroll
-    for (int c = 8; c >= 0; --c) {
-#pragma unroll
-        for (int i = 0; i < N; ++i) {
-            pe[i] = fma(pe[i], re[i], kP[c]);
-            pm[i] = fma(pm[i], rm[i], kP[c]);
-        }
-    }
-    double E[N], G[N], eg[N], den[N], rc[N], s[N], w[N], R[N];
+    double eg[N], den[N], rc[N], s[N], w[N], R[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-        E[i] = ldexp(fma(re[i] * re[i], pe[i], re[i]) + 1.0, (int)ke[i]);  // exp(-(M - m))
-        const double tk = ldexp(1.0, (int)km[i]);
-        G[i] = -fma(tk, fma(rm[i] * rm[i], pm[i], rm[i]), tk - 1.0);  // -expm1(-2m)
         eg[i] = E[i] * G[i];
         den[i] = fma(2.0, E[i], 2.0) - eg[i];  // in [2, 4]
         rc[i] = __builtin_amdgcn_rcp(den[i]);
@@ -531,7 +554,8 @@ __device__ __forceinline__ void f_exact_pm_n(const double* x, const double* y, d
 #pragma unroll
     for (int i = 0; i < N; ++i) {
         const double v = m[i] + fma(s[i] * w[i], R[i], s[i] + s[i]);
-        out[i] = neg[i] ? -v : v;
+        const unsigned long long vb = (unsigned long long)__double_as_longlong(v);
+        out[i] = __longlong_as_double((long long)(vb ^ ((unsigned long long)sg[i] << 32)));
     }
 }
 __device__ __forceinline__ double f_exact_pm(double x, double y, double lmax) {

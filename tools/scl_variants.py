@@ -27,7 +27,9 @@ def build(specs):
     def one(spec):
         name, flags = spec.split(":", 1)
         base = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-DPL_DEV=1", *flags.split()]
-        src = os.path.join(b.CSRC, "scl_tree_kernel.hip")
+        # SCL_VARIANT_SRC: another copy of the kernel source (in csrc/, for its includes), e.g. the
+        # committed version (git show HEAD:... > csrc/_head_scl_tree_kernel.hip) against the working tree
+        src = os.path.join(b.CSRC, os.environ.get("SCL_VARIANT_SRC", "scl_tree_kernel.hip"))
         o1, o2 = os.path.join(VAR, f"sclt_{name}_L8.o"), os.path.join(VAR, f"sclt_{name}_disp.o")
         subprocess.check_call(base + ["-DPL_SCL_TREE_L=8", "-c", src, "-o", o1])
         subprocess.check_call(base + ["-DPL_SCL_TREE_DISPATCH", "-DPL_SCL_VARIANT_ONLY_L8", "-c", src, "-o", o2])
@@ -106,7 +108,9 @@ def time_all(n=1024, k=512, bs=8192, reps=5, rounds=2):
             if ref is None:
                 ref = (out.clone(), pm.clone())
             same = torch.equal(out, ref[0]) and torch.equal(pm, ref[1])
-            print(f"round {rnd} {name:16s} {ms:8.3f} ms  {bs / ms / 1e3:7.4f} Mcw/s  identical={same}", flush=True)
+            rows = int((out != ref[0]).any(1).sum())  # rows whose bits differ from the first library's
+            print(f"round {rnd} {name:16s} {ms:8.3f} ms  {bs / ms / 1e3:7.4f} Mcw/s  identical={same} rows_differing={rows}",
+                  flush=True)
 
 
 if __name__ == "__main__":
