@@ -145,8 +145,11 @@ struct Prof {
         (P).t = prof_n;                                              \
     } while (0)
 #define PROF_MARK(i) PROF_MARK_P(prof, i)
-// sub-phases of the exact-f virtual pass (vvisit_ex), reported in the slots the FAST kernels leave
-// empty: 8 = cache / channel loads (waited for), 10 = the four-outcome f, 11 = the per-path levels
+#endif
+#if PL_SCL_PROF >= 2
+// PL_SCL_PROF 2: sub-phases of the exact-f virtual pass (vvisit_ex), reported in the slots the FAST
+// kernels leave empty: 8 = cache / channel loads (waited for), 10 = the four-outcome f, 11 = the
+// per-path levels (the waits and LDS counters perturb the timing: for shares only)
 __shared__ unsigned long long vex_prof[3];
 #define VEX_T0 unsigned long long vex_t = __builtin_amdgcn_s_memtime()
 #define VEX_MARK(i)                                                            \
@@ -155,13 +158,16 @@ __shared__ unsigned long long vex_prof[3];
         if (lane == 0) vex_prof[i] += vex_n - vex_t;                           \
         vex_t = vex_n;                                                         \
     } while (0)
+#else
+#define VEX_T0
+#define VEX_MARK(i)
+#endif
+#if PL_SCL_PROF
 #define PROF_PARAM , Prof& prof
 #define PROF_ARG , prof
 #else
 #define PROF_DECL
 #define PROF_MARK(i)
-#define VEX_T0
-#define VEX_MARK(i)
 #define PROF_PARAM
 #define PROF_ARG
 #endif
@@ -1015,7 +1021,7 @@ __device__ PL_FEX_PASS_ATTR void vvisit_ex(const float* __restrict__ llr, int64_
                 }
             }
         }
-#if PL_SCL_PROF
+#if PL_SCL_PROF >= 2
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         VEX_MARK(0);
 #endif
@@ -2247,7 +2253,7 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
     pl::sp_load_tables(lane, 64);  // the penalty's log table (softplus.h, PL_SP_FORM 3)
     pl::fex_load_table<FM == 1>(lane);  // the exact f's 2^(j/64) table (softplus.h, PL_FEX_TAB)
     PROF_DECL;
-#if PL_SCL_PROF
+#if PL_SCL_PROF >= 2
     if (lane < 3) vex_prof[lane] = 0ull;
     __syncthreads();
 #endif
@@ -2493,11 +2499,13 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
     }
 #if PL_SCL_PROF
     PROF_MARK(7);
+#if PL_SCL_PROF >= 2
     if constexpr (FM == 1 && FAST) {  // the vvisit_ex sub-phases (inside slot 0's time)
         prof.acc[8] = vex_prof[0];
         prof.acc[10] = vex_prof[1];
         prof.acc[11] = vex_prof[2];
     }
+#endif
     if (out_pm != nullptr && lane < kProfSlots) {
         unsigned long long v = prof.acc[0];
 #pragma unroll
