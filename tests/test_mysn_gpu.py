@@ -100,6 +100,32 @@ def test_mysn_scl_random_code_vs_oracle(pa, log_n, L, fast):
     assert np.abs(pm.cpu().numpy()[ok] - wpm[ok]).max() < 1e-6
 
 
+@pytest.mark.parametrize("lmax", [7.5, 100.0, 300.0])
+@pytest.mark.parametrize("kernel", ["subtree", "generic"])
+def test_mysn_scl_exact_f_llr_max_vs_oracle(pa, lmax, kernel):
+    """Exact f at llr_max far from 30 (my_sn dec.py:213): the f's exponentials take arguments down
+    to -2 llr_max (softplus.h fex_exp: the 2^(j/64) table and the shifter's integer range), the clip
+    folds into min(|x|, llr_max).  Strong channel LLRs so the clip binds at 7.5 and node values
+    reach hundreds.  (Above llr_max ~355 the reference's own float64 exp(xc + yc) overflows and its
+    f turns +inf where ours stays finite: DESIGN.md section 7.)  Row mismatches against the C oracle
+    within the P0_SCL gate, metrics to 1e-6 on agreeing rows, on both SCL kernels, fast-SCL on."""
+    from polar_amd import _lib, ops
+    k, n, L, bs = 128, 256, 8, 64
+    rng = np.random.default_rng(int(lmax) + (kernel == "generic"))
+    fp = pa.reference_frozen_pos(k, n).numpy()
+    u = rng.integers(0, 2, (bs, k)).astype(np.float32)
+    cw = oracle.polar_encode(u, fp, n)
+    llr = ((2 * cw - 1) * 6.0 + rng.standard_normal(cw.shape) * 3.0).astype(np.float32)
+    flags = _lib.PL_PLAN_FAST_SCL | (_lib.PL_PLAN_GENERIC if kernel == "generic" else 0)
+    want, wpm = oracle.scl_decode_mysn(llr, fp, L, fast_scl=True, exact_f=True, llr_max=lmax)
+    plan = _lib.Plan(n, pa.frozen_mask(fp, n), L, _lib.PL_F_EXACT, llr_max=lmax, flags=flags)
+    got, pm = ops.scl_decode(plan, torch.from_numpy(llr).cuda(), return_pm=True)
+    ok = (got.cpu().numpy() == want).all(1)
+    assert binom_upper_ok(int((~ok).sum()), len(ok), P0_SCL), ok.mean()
+    assert np.abs(pm.cpu().numpy()[ok] - wpm[ok]).max() < 1e-6
+    assert np.isfinite(pm.cpu().numpy()).all()
+
+
 def test_mysn_scl_minsum_fast_is_exact_vs_oracle(pa):
     """Fast-SCL with the min-sum f has no transcendental in the tree: bits must be identical."""
     from polar_amd import _lib, ops
