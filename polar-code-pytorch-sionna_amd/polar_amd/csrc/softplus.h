@@ -146,6 +146,10 @@ __device__ __forceinline__ double pm_log(double y) {  // y >= 1, finite
 //   s = f / (2 + f): a reciprocal, PL_RCP_STEPS Newton steps and a residual correction (denominator in
 //   [1.41, 2.83]) instead of the scaled IEEE division sequence.
 // 7 fewer FMAs and a shorter division than the Taylor forms above, same accuracy class (~1 ulp).
+#ifndef PL_SP_ASM
+#define PL_SP_ASM 1  // the Estrin polynomials as asm blocks of VOP3 FMAs: A/B 0.734 -> 0.714 ms min-sum SCL,
+                    // bit-identical (profiles/r06zd_spasm_ab2.txt); 0: plain fma()
+#endif
 #ifndef PL_SP_FORM
 #define PL_SP_FORM 2  // A/B r03l: 0.990 vs 1.000 ms (min-sum), 1.050 vs 1.113 ms (min-sum fast-SCL)
 #endif
@@ -165,7 +169,27 @@ __device__ __forceinline__ double pm_exp_e(double z) {
     r = fma(-k, kLn2Lo, r);
     const double r2 = r * r;
     double P;
-    if constexpr (ESTRIN) {
+    if constexpr (ESTRIN && PL_SP_ASM) {
+        // the same operations as below, each first-level pair as a VOP3 FMA with its multiplier in
+        // an SGPR and its addend in a VGPR: left to itself the compiler uses the two-address
+        // v_fmac_f64 and copies the (loop-invariant) addend into the destination first -- one
+        // v_mov_b64 per pair; one block, so no hazard padding between the steps
+        double a, b, c, d, e, r4, ab, cd, t;
+        asm("v_fma_f64 %0, %9, %11, %12\n\t"
+            "v_fma_f64 %1, %9, %13, %14\n\t"
+            "v_fma_f64 %2, %9, %15, %16\n\t"
+            "v_fma_f64 %3, %9, %17, %18\n\t"
+            "v_fma_f64 %4, %9, %19, %20\n\t"
+            "v_mul_f64 %5, %10, %10\n\t"
+            "v_fma_f64 %6, %0, %10, %1\n\t"
+            "v_fma_f64 %7, %2, %10, %3\n\t"
+            "v_fma_f64 %8, %6, %5, %7\n\t"
+            "v_fma_f64 %8, %8, %10, %4"
+            : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d), "=&v"(e), "=&v"(r4), "=&v"(ab), "=&v"(cd), "=&v"(t)
+            : "v"(r), "v"(r2), "s"(kSpP[9]), "v"(kSpP[8]), "s"(kSpP[7]), "v"(kSpP[6]), "s"(kSpP[5]),
+              "v"(kSpP[4]), "s"(kSpP[3]), "v"(kSpP[2]), "s"(kSpP[1]), "v"(kSpP[0]));
+        P = t;
+    } else if constexpr (ESTRIN) {
         const double a = fma(kSpP[9], r, kSpP[8]), b = fma(kSpP[7], r, kSpP[6]), c = fma(kSpP[5], r, kSpP[4]);
         const double d = fma(kSpP[3], r, kSpP[2]), e = fma(kSpP[1], r, kSpP[0]);
         const double r4 = r2 * r2;
@@ -211,7 +235,21 @@ __device__ __forceinline__ double pm_log_e(double y) {  // y >= 1, finite
     const double s = fma(rc, fma(-den, q, f), q);
     const double z = s * s;
     double R;
-    if constexpr (ESTRIN) {
+    if constexpr (ESTRIN && PL_SP_ASM) {  // as in pm_exp_e: VOP3 FMAs, no addend copies
+        double p01, p23, p45, z2, z4, u, v;
+        asm("v_fma_f64 %0, %7, %8, %9\n\t"
+            "v_fma_f64 %1, %7, %10, %11\n\t"
+            "v_fma_f64 %2, %7, %12, %13\n\t"
+            "v_mul_f64 %3, %7, %7\n\t"
+            "v_mul_f64 %4, %3, %3\n\t"
+            "v_fma_f64 %5, %3, %14, %2\n\t"
+            "v_fma_f64 %6, %1, %3, %0\n\t"
+            "v_fma_f64 %5, %5, %4, %6"
+            : "=&v"(p01), "=&v"(p23), "=&v"(p45), "=&v"(z2), "=&v"(z4), "=&v"(u), "=&v"(v)
+            : "v"(z), "s"(kSpRL[1]), "v"(kSpRL[0]), "s"(kSpRL[3]), "v"(kSpRL[2]), "s"(kSpRL[5]),
+              "v"(kSpRL[4]), "s"(kSpRL[6]));
+        R = u;
+    } else if constexpr (ESTRIN) {
         const double p01 = fma(kSpRL[1], z, kSpRL[0]), p23 = fma(kSpRL[3], z, kSpRL[2]);
         const double p45 = fma(kSpRL[5], z, kSpRL[4]);
         const double z2 = z * z, z4 = z2 * z2;
