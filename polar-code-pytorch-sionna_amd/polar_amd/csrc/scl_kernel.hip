@@ -368,7 +368,7 @@ __global__ __launch_bounds__(64) void scl_decode_kernel(const float* __restrict_
     const int lane = threadIdx.x;
     const int64_t b = blockIdx.x;
     pl::sp_load_tables(lane, 64);  // the penalty's log table (softplus.h, PL_SP_FORM 3)
-    pl::fex_load_table<FM == 1>(lane);  // the exact f's 2^(j/64) table (softplus.h, PL_FEX_TAB)
+    pl::fex_load_table<FM == 1>(lane);  // the exact f's 2^(j/64) table (softplus.h fex_exp)
     St t;
     t.A = reinterpret_cast<double*>(smem + y.off_alpha);
     t.ch = reinterpret_cast<float*>(smem + y.off_ch);

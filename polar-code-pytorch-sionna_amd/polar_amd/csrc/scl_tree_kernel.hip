@@ -874,14 +874,15 @@ __device__ void vvisit64(const St& t, int pos, bool is_g, int lane, const int* w
 #endif
 }
 
-// One pass of a virtual node for the exact f (FM = 1, any V >= 1), where an f costs ~70 VALU and
+// One pass of a virtual node for the exact f (FM = 1, any V >= 1), where an f costs ~65 VALU and
 // dominates: the leading f levels (from the channel down to the first g) are path-independent, so
-// each lane evaluates them once per (codeword, element) and only the levels below the first g
-// once per path -- 2.1x fewer f evaluations than the per-path recursion at n = 1024.  Every level
-// is a loop with a uniform trip count over register arrays indexed by the (uniform) loop counter
-// (s_set_gpr_idx, no scratch), so each f appears a handful of times in the code instead of once
-// per tree position (the unrolled form does not fit the register budget or the instruction cache
-// with a 70-instruction f).  Level q (stage s + q) combines v[m] and v[m + 2^q], m < 2^q: f when
+// each lane evaluates them once per (codeword, element) -- from the workspace's leftmost-chain
+// cache and four-outcome tables -- and only the levels below the first g once per path: 2.1x
+// fewer f evaluations than the per-path recursion at n = 1024.  The per-path levels are unrolled
+// blocks with compile-time register indices (vex_levels); at V = 4 only levels 1 and 0 can be f
+// levels, so the f appears three times per path block.  (Until round 6 they were loops indexing
+// register vectors with the uniform loop counter, which the backend lowered to compare-and-select
+// chains over every entry.)  Level q (stage s + q) combines v[m] and v[m + 2^q], m < 2^q: f when
 // the stage-(s+q) node is a left child, else g with bit base[q] + m 2^s of the path.  The same
 // operands and operations as vtree(), so the same values.
 #ifndef PL_SCL_VPF
@@ -898,7 +899,7 @@ __device__ __forceinline__ void vex_levels(F& level) {  // level(Q), level(Q - 1
     }
 }
 #ifndef PL_SCL_FEX_INL
-#define PL_SCL_FEX_INL 1  // 1: vvisit_ex inlined (register arrays via s_set_gpr_idx); 0: out of line (A/B r03i:
+#define PL_SCL_FEX_INL 1  // 1: vvisit_ex inlined (its register blocks in the kernel's registers); 0: out of line (A/B r03i:
                           // callee register saves through scratch every pass, 4.10 vs 3.71 ms)
 #endif
 #if PL_SCL_FEX_INL
@@ -2251,7 +2252,7 @@ void scl_tree_kernel(const float* __restrict__ llr, int64_t bs, void* __restrict
     const int gl = lane & (GW - 1), my_c = lane / GW;
     const Cw mine = t.cw(my_c);
     pl::sp_load_tables(lane, 64);  // the penalty's log table (softplus.h, PL_SP_FORM 3)
-    pl::fex_load_table<FM == 1>(lane);  // the exact f's 2^(j/64) table (softplus.h, PL_FEX_TAB)
+    pl::fex_load_table<FM == 1>(lane);  // the exact f's 2^(j/64) table (softplus.h fex_exp)
     PROF_DECL;
 #if PL_SCL_PROF >= 2
     if (lane < 3) vex_prof[lane] = 0ull;
